@@ -1,0 +1,119 @@
+"""Deterministic random-init merged checkpoints (no network => no ImageNet weights).
+
+``merged_state_dict(seed, n_heads, distinct_backbones)`` returns a state dict in
+the reference's merged-checkpoint layout (``model_merger.py:154-159``;
+SURVEY.md Appendix B): ``sub_models.<i>.base.<timm key>`` and
+``sub_models.<i>.head.<idx>.<param>``.
+
+Values come from a counter-based hash (sad.synth.mix64) turned into
+Irwin-Hall(4) normals with exact float64 arithmetic, so they regenerate
+bit-identically on any host.  BatchNorm running statistics default to (0, 1);
+tests and the bench overlay calibrated statistics (tests/golden/bn_stats_*.npz)
+so that activations stay O(1) through the 20 conv layers.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from .synth import GOLD, GOLD2, mix64
+
+BLOCK_CHANNELS = (64, 128, 256, 512)
+
+
+def _normals(seed: int, tag: int, n: int) -> np.ndarray:
+    key = mix64((mix64(seed & 0xFFFFFFFFFFFFFFFF) + tag * GOLD) & 0xFFFFFFFFFFFFFFFF)
+    j = np.arange(n, dtype=np.uint64)
+    r = mix64(np.uint64(key) + (j + np.uint64(1)) * np.uint64(GOLD2))
+    s = np.zeros(n, dtype=np.int64)
+    for sh in (0, 16, 32, 48):
+        s += ((r >> np.uint64(sh)) & np.uint64(0xFFFF)).astype(np.int64)
+    return (s - 131070).astype(np.float64) / 37837.23
+
+
+def backbone_param_shapes(layers=(2, 2, 2, 2)):
+    """Ordered (timm key, shape, kind) for a BasicBlock ResNet; kind in
+    {conv, bn}.  Mirrors timm's state-dict order."""
+    out = [('conv1', (64, 3, 7, 7), 'conv'), ('bn1', (64,), 'bn')]
+    inplanes = 64
+    for li, (planes, n) in enumerate(zip(BLOCK_CHANNELS, layers)):
+        for b in range(n):
+            s = (1 if li == 0 else 2) if b == 0 else 1
+            p = f'layer{li + 1}.{b}'
+            out.append((f'{p}.conv1', (planes, inplanes, 3, 3), 'conv'))
+            out.append((f'{p}.bn1', (planes,), 'bn'))
+            out.append((f'{p}.conv2', (planes, planes, 3, 3), 'conv'))
+            out.append((f'{p}.bn2', (planes,), 'bn'))
+            if b == 0 and (s != 1 or inplanes != planes):
+                out.append((f'{p}.downsample.0', (planes, inplanes, 1, 1), 'conv'))
+                out.append((f'{p}.downsample.1', (planes,), 'bn'))
+            inplanes = planes
+    return out
+
+
+HEAD_LAYOUT = [(2, 'linear', (512, 512)), (3, 'bn', (512,)), (6, 'linear', (256, 512)),
+               (7, 'bn', (256,)), (10, 'linear', (2, 256))]
+
+
+def _bn(seed, tag, c, prefix, sd):
+    sd[f'{prefix}.weight'] = torch.from_numpy((1.0 + 0.1 * _normals(seed, tag, c)).astype(np.float32))
+    sd[f'{prefix}.bias'] = torch.from_numpy((0.1 * _normals(seed, tag + 1, c)).astype(np.float32))
+    sd[f'{prefix}.running_mean'] = torch.zeros(c)
+    sd[f'{prefix}.running_var'] = torch.ones(c)
+    sd[f'{prefix}.num_batches_tracked'] = torch.tensor(0, dtype=torch.long)
+
+
+def backbone_state_dict(seed: int) -> "OrderedDict[str, torch.Tensor]":
+    sd = OrderedDict()
+    for t, (key, shape, kind) in enumerate(backbone_param_shapes()):
+        tag = 1000 + 4 * t
+        if kind == 'conv':
+            fan_out = shape[0] * shape[2] * shape[3]
+            std = (2.0 / fan_out) ** 0.5
+            w = (_normals(seed, tag, int(np.prod(shape))) * std).astype(np.float32).reshape(shape)
+            sd[f'{key}.weight'] = torch.from_numpy(w)
+        else:
+            _bn(seed, tag, shape[0], key, sd)
+    return sd
+
+
+def head_state_dict(seed: int) -> "OrderedDict[str, torch.Tensor]":
+    sd = OrderedDict()
+    for t, (idx, kind, shape) in enumerate(HEAD_LAYOUT):
+        tag = 9000 + 4 * t
+        if kind == 'linear':
+            fan_in = shape[1]
+            w = (_normals(seed, tag, shape[0] * shape[1]) / np.sqrt(fan_in)).astype(np.float32)
+            sd[f'{idx}.weight'] = torch.from_numpy(w.reshape(shape))
+            sd[f'{idx}.bias'] = torch.from_numpy((0.05 * _normals(seed, tag + 1, shape[0])).astype(np.float32))
+        else:
+            _bn(seed, tag, shape[0], str(idx), sd)
+    return sd
+
+
+def merged_state_dict(seed: int = 0, n_heads: int = 6, distinct_backbones: bool = False,
+                      bn_stats: dict | None = None) -> "OrderedDict[str, torch.Tensor]":
+    """Merged checkpoint state dict.  Sub-model i uses backbone seed
+    ``seed + (i if distinct_backbones else 0)`` (shared backbone = the reference's
+    quirk C2 situation) and head seed ``seed * 1000 + i + 1``.  ``bn_stats`` maps
+    full keys (``sub_models.i....running_mean``) to arrays overriding defaults."""
+    sd = OrderedDict()
+    for i in range(n_heads):
+        bb = backbone_state_dict(seed + (i if distinct_backbones else 0))
+        for k, v in bb.items():
+            sd[f'sub_models.{i}.base.{k}'] = v.clone()
+        hd = head_state_dict(seed * 1000 + i + 1)
+        for k, v in hd.items():
+            sd[f'sub_models.{i}.head.{k}'] = v.clone()
+    if bn_stats:
+        for k, v in bn_stats.items():
+            if k in sd:
+                sd[k] = torch.as_tensor(np.asarray(v), dtype=sd[k].dtype).reshape(sd[k].shape)
+    return sd
+
+
+def load_bn_stats(path) -> dict:
+    z = np.load(path, allow_pickle=False)
+    return {k: z[k] for k in z.files}
