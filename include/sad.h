@@ -1,0 +1,157 @@
+/*
+ * sad.h -- C ABI of libsad.so, the MI355X (gfx950) hot path of the
+ * synthetic-audio-detection pipeline:
+ *
+ *   int16 PCM (4 s @ 32 kHz) -> STFT -> mel -> dB -> standardise      [frontend]
+ *   -> bilinear 512x512 -> ResNet-18 backbone -> global avg pool        [backbone]
+ *   -> N binary heads -> real-logit-averaging ensemble merge            [heads]
+ *
+ * The reference (TtesseractT/Synthetic-Audio-Detection @ 2025-05-23) has no
+ * FFI: its hot path is Python calling torchaudio / torchvision / timm.  Each
+ * entry point below names the reference interface (file:line) it replaces; the
+ * Python host layer (synthetic-audio-detection_amd/sad/_lib.py) binds them with
+ * ctypes, exactly as INTEGRATION.md shows.
+ *
+ * Conventions:
+ *   - every call returns 0 on success, a negative sad_status otherwise;
+ *     sad_last_error() returns a thread-local message for the last failure;
+ *   - all tensors are caller-owned device pointers (PyTorch caching allocator);
+ *     the library never frees caller memory;
+ *   - plans are opaque, immutable after creation, freed by *_destroy;
+ *   - *_run calls are asynchronous on the given hipStream_t (passed as void*),
+ *     never allocate, never synchronise (graph-capturable);
+ *   - distinct plans / streams may be used from different threads.
+ */
+#ifndef SAD_H_
+#define SAD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum sad_status {
+  SAD_OK = 0,
+  SAD_ERR_ARG = -1,      /* bad argument / shape */
+  SAD_ERR_HIP = -2,      /* HIP runtime error */
+  SAD_ERR_STATE = -3,    /* not initialised / wrong plan */
+  SAD_ERR_NOMEM = -4,    /* workspace too small or device allocation failed */
+};
+
+enum sad_dtype {
+  SAD_F32 = 0,   /* fp32 activations, f32 MFMA (v_mfma_f32_16x16x4_f32): parity mode */
+  SAD_BF16 = 1,  /* bf16 activations, bf16 MFMA (v_mfma_f32_16x16x32_bf16), f32 accumulate */
+};
+
+/* ---------------------------------------------------------------- runtime */
+/* Select the device for this thread's subsequent plan creation. */
+int sad_init(int device);
+const char* sad_last_error(void);
+/* Library / kernel build identification (for provenance in bench output). */
+const char* sad_version(void);
+
+/* --------------------------------------------------------------- frontend */
+/* Replaces torchaudio.transforms.MelSpectrogram + AmplitudeToDB + the
+ * standardisation at inference_runner.py:157-171 (and the norm=None trainer
+ * variant at submodel_trainer.py:97-105,191-199). */
+typedef struct sad_frontend_cfg {
+  int32_t sample_rate;   /* 32000 */
+  int32_t n_fft;         /* 2048 (only value supported) */
+  int32_t hop_length;    /* 512 */
+  int32_t n_mels;        /* 128 */
+  float f_min;           /* 20 */
+  float f_max;           /* 12000 */
+  int32_t norm_slaney;   /* 1 = 'slaney' (inference), 0 = None (trainer) */
+  float top_db;          /* 80; <0 disables the clamp */
+  int32_t n_samples;     /* samples per segment, 128000 */
+} sad_frontend_cfg;
+
+typedef struct sad_frontend_plan sad_frontend_plan;
+
+int sad_frontend_plan_create(const sad_frontend_cfg* cfg, sad_frontend_plan** out);
+int sad_frontend_plan_destroy(sad_frontend_plan* plan);
+/* Number of STFT frames per segment (1 + n_samples / hop = 251). */
+int sad_frontend_frames(const sad_frontend_plan* plan, int32_t* n_frames);
+
+/* pcm: int16 mono segments, segment i at pcm + i*seg_stride (elements),
+ *      n_samples each (stereo callers average on the host first);
+ * out_db:  optional [n_seg, n_mels, n_frames] fp32 dB map after the top-db
+ *          clamp (NULL to skip);
+ * out_map: [n_seg, n_mels, n_frames] fp32 standardised map
+ *          (x - mean) / (std_unbiased + 1e-6), per segment. */
+int sad_frontend_run(const sad_frontend_plan* plan, const int16_t* pcm, int64_t n_seg,
+                     int64_t seg_stride, float* out_db, float* out_map, void* stream);
+
+/* Replaces torchvision.transforms.Resize((512,512)) + repeat(3,1,1)
+ * (inference_runner.py:172-174) for callers that want the image itself:
+ * map [n, h, w] fp32 -> img [n, out_h, out_w] in `dtype` (one channel: the
+ * reference's three channels are identical and are folded into conv1). */
+int sad_resize_run(const float* map, int64_t n, int32_t h, int32_t w, int32_t out_h,
+                   int32_t out_w, int32_t dtype, void* img, void* stream);
+
+/* --------------------------------------------------------------- backbone */
+/* Replaces timm.create_model('resnet18', num_classes=0).forward_features +
+ * head[0:2] (AdaptiveAvgPool2d + Flatten) at inference_runner.py:35,49-51:
+ * standardised map -> (fused) resize -> ResNet-18 -> pooled [B, 512] fp32. */
+typedef struct sad_backbone_plan sad_backbone_plan;
+
+/* params: host fp32 arrays in timm state-dict order, for each conv:
+ *   conv weight [Cout, Cin, KH, KW], then its BN: weight, bias, running_mean,
+ *   running_var  (5 pointers per conv+BN; conv1 has Cin = 3).
+ * Order: conv1/bn1, then for layer1..4, block 0..1: conv1/bn1, conv2/bn2,
+ * [downsample.0/downsample.1 for block 0 of layer2..4].  n_params must be
+ * 5 * 20 = 100.  BN is folded (eps 1e-5) and weights are re-laid out
+ * [Cout][KH][KW][Cin] in `dtype` on the current device. */
+int sad_backbone_plan_create(const float* const* params, int32_t n_params, int32_t dtype,
+                             int32_t map_h, int32_t map_w, sad_backbone_plan** out);
+int sad_backbone_plan_destroy(sad_backbone_plan* plan);
+/* Device workspace bytes needed by sad_backbone_run for a micro-batch of
+ * `micro_batch` segments (the run processes B in chunks of micro_batch). */
+int sad_backbone_workspace_size(const sad_backbone_plan* plan, int64_t micro_batch, size_t* bytes);
+/* map: [B, map_h, map_w] fp32 standardised maps; feats: [B, 512] fp32. */
+int sad_backbone_run(const sad_backbone_plan* plan, const float* map, int64_t B,
+                     int64_t micro_batch, float* feats, void* workspace, size_t ws_bytes,
+                     void* stream);
+/* Debug/parity entry: run only the fused resize+stem (conv1+bn1+relu+maxpool)
+ * on B maps, writing NHWC [B,128,128,64] in the plan's dtype. */
+int sad_backbone_stem_run(const sad_backbone_plan* plan, const float* map, int64_t B,
+                          void* out, void* stream);
+/* Debug/parity entry: layer4 output NHWC [B,16,16,512] (plan dtype) for B <=
+ * micro_batch, in addition to the pooled features. */
+int sad_backbone_run_debug(const sad_backbone_plan* plan, const float* map, int64_t B,
+                           float* feats, void* layer4_out, void* workspace, size_t ws_bytes,
+                           void* stream);
+
+/* ------------------------------------------------------------------ heads */
+/* Replaces BinaryClassifier.head (inference_runner.py:36-48) for N sub-models
+ * and ModularMultiHeadClassifier.forward (inference_runner.py:62-73).
+ * params: per head, host fp32, in nn.Sequential index order:
+ *   2.weight [512,512], 2.bias, 3.{weight,bias,running_mean,running_var},
+ *   6.weight [256,512], 6.bias, 7.{weight,bias,running_mean,running_var},
+ *   10.weight [2,256], 10.bias            (14 pointers per head)
+ * feat_index[h]: which backbone's pooled features head h reads (0..n_feat-1). */
+typedef struct sad_heads_plan sad_heads_plan;
+
+int sad_heads_plan_create(const float* const* params, int32_t n_heads, const int32_t* feat_index,
+                          int32_t n_feat, sad_heads_plan** out);
+int sad_heads_plan_destroy(sad_heads_plan* plan);
+int sad_heads_workspace_size(const sad_heads_plan* plan, int64_t B, size_t* bytes);
+/* feats: n_feat pointers to [B,512] fp32; logits: [B, N, 2] fp32 (per head
+ * [Real, Synthetic]); merged: [B, N+1] fp32 = [syn_1..syn_N, mean_i real_i]. */
+int sad_heads_merge_run(const sad_heads_plan* plan, const float* const* feats, int64_t B,
+                        float* logits, float* merged, void* workspace, size_t ws_bytes,
+                        void* stream);
+
+/* -------------------------------------------------------------- synthetic */
+/* Deterministic synthetic segments; bit-identical to
+ * sad/synth.py up to rare 1-LSB float64 libm differences in the tone term.
+ * pcm: [count, n_samples] int16, segments first_seg .. first_seg+count-1. */
+int sad_synth_pcm(uint64_t seed, int64_t first_seg, int64_t count, int32_t n_samples,
+                  int16_t* pcm, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAD_H_ */

@@ -1,0 +1,453 @@
+// api.hip -- C ABI of libsad.so: runtime, backbone and heads plans.
+// Declarations and the reference interfaces each entry replaces: include/sad.h.
+#include <math.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace sad {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+// ResNet-18 conv table in timm state-dict order.
+struct ConvSpec {
+  int cin, cout, k, stride, pad;
+};
+static std::vector<ConvSpec> resnet18_specs() {
+  std::vector<ConvSpec> v;
+  v.push_back({3, 64, 7, 2, 3});  // conv1
+  int inp = 64;
+  const int planes[4] = {64, 128, 256, 512};
+  for (int li = 0; li < 4; ++li) {
+    for (int b = 0; b < 2; ++b) {
+      const int s = (b == 0 && li > 0) ? 2 : 1;
+      v.push_back({inp, planes[li], 3, s, 1});          // conv1
+      v.push_back({planes[li], planes[li], 3, 1, 1});   // conv2
+      if (b == 0 && (s != 1 || inp != planes[li])) v.push_back({inp, planes[li], 1, s, 0});  // downsample
+      inp = planes[li];
+    }
+  }
+  return v;
+}
+
+struct DevConv {
+  ConvSpec spec;
+  void* w = nullptr;      // [cout][k][k][cin] dtype
+  float* bias = nullptr;  // [cout]
+};
+
+}  // namespace sad
+
+using namespace sad;
+
+struct sad_backbone_plan {
+  int dtype;
+  int mh, mw;
+  int device;
+  void* stem_w = nullptr;
+  float* stem_b = nullptr;
+  std::vector<DevConv> convs;  // index 1.. of the spec table
+};
+
+struct sad_heads_plan {
+  int n_heads, n_feat;
+  int device;
+  std::vector<int> feat_index;
+  std::vector<int> group_of;      // head -> group (== feat index order of appearance)
+  std::vector<int> y1_col;        // head -> column offset in Y1
+  std::vector<std::vector<int>> groups;  // feat -> heads
+  std::vector<float*> w1;          // per group: [512*G][512] folded
+  std::vector<float*> b1;          // per group: [512*G]
+  float* w2 = nullptr;             // [N][256][512] folded
+  float* b2 = nullptr;             // [N][256]
+  float* w3 = nullptr;             // [N][2][256]
+  float* b3 = nullptr;             // [N][2]
+};
+
+extern "C" const char* sad_last_error(void) { return g_err.c_str(); }
+extern "C" const char* sad_version(void) { return "libsad 0.1 gfx950 (" __DATE__ " " __TIME__ ")"; }
+
+extern "C" int sad_init(int device) {
+  int n = 0;
+  SAD_CHECK_HIP(hipGetDeviceCount(&n));
+  SAD_REQUIRE(device >= 0 && device < n, "device index out of range");
+  SAD_CHECK_HIP(hipSetDevice(device));
+  return SAD_OK;
+}
+
+// ------------------------------------------------------------- folding ----
+static void fold_bn(const float* g, const float* beta, const float* mu, const float* var, int c,
+                    std::vector<double>& scale, std::vector<double>& shift) {
+  scale.resize(c);
+  shift.resize(c);
+  for (int i = 0; i < c; ++i) {
+    scale[i] = (double)g[i] / sqrt((double)var[i] + 1e-5);
+    shift[i] = (double)beta[i] - (double)mu[i] * scale[i];
+  }
+}
+
+template <typename V>
+static int upload(void** dst, const std::vector<V>& v) {
+  SAD_CHECK_HIP(hipMalloc(dst, v.size() * sizeof(V)));
+  SAD_CHECK_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(V), hipMemcpyHostToDevice));
+  return SAD_OK;
+}
+
+static int upload_typed(void** dst, const std::vector<double>& v, int dtype) {
+  if (dtype == SAD_BF16) {
+    std::vector<u16> h(v.size());
+    for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_host((float)v[i]);
+    return upload(dst, h);
+  }
+  std::vector<float> h(v.size());
+  for (size_t i = 0; i < v.size(); ++i) h[i] = (float)v[i];
+  return upload(dst, h);
+}
+
+extern "C" int sad_backbone_plan_create(const float* const* params, int32_t n_params, int32_t dtype,
+                                        int32_t map_h, int32_t map_w, sad_backbone_plan** out) {
+  const std::vector<ConvSpec> specs = resnet18_specs();
+  SAD_REQUIRE(params && out, "null params/out");
+  SAD_REQUIRE(n_params == (int)specs.size() * 5, "n_params must be 100 (20 conv+BN groups)");
+  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
+  SAD_REQUIRE(map_h > 0 && map_w > 0, "map shape");
+  for (int i = 0; i < n_params; ++i) SAD_REQUIRE(params[i] != nullptr, "null parameter pointer");
+  auto* p = new sad_backbone_plan();
+  p->dtype = dtype;
+  p->mh = map_h;
+  p->mw = map_w;
+  (void)hipGetDevice(&p->device);
+  std::vector<double> sc, sh;
+  int rc;
+  // stem: fold BN and the 3 identical input channels; k = ky*7+kx padded to 64
+  {
+    const float* W = params[0];
+    fold_bn(params[1], params[2], params[3], params[4], 64, sc, sh);
+    std::vector<double> w(64 * 64, 0.0), b(64);
+    for (int co = 0; co < 64; ++co) {
+      for (int k = 0; k < 49; ++k) {
+        double s = 0.0;
+        for (int c = 0; c < 3; ++c) s += (double)W[(co * 3 + c) * 49 + k];
+        const int pos = dtype == SAD_BF16 ? k : ((k & 3) * 16 + (k >> 2));  // f32: k=4q+g at g*16+q
+        w[co * 64 + pos] = s * sc[co];
+      }
+      b[co] = sh[co];
+    }
+    if ((rc = upload_typed(&p->stem_w, w, dtype))) return rc;
+    std::vector<float> bf(b.begin(), b.end());
+    if ((rc = upload((void**)&p->stem_b, bf))) return rc;
+  }
+  for (size_t ci = 1; ci < specs.size(); ++ci) {
+    const ConvSpec& s = specs[ci];
+    const float* W = params[ci * 5];
+    fold_bn(params[ci * 5 + 1], params[ci * 5 + 2], params[ci * 5 + 3], params[ci * 5 + 4], s.cout, sc, sh);
+    std::vector<double> w((size_t)s.cout * s.k * s.k * s.cin);
+    for (int co = 0; co < s.cout; ++co)
+      for (int c = 0; c < s.cin; ++c)
+        for (int ky = 0; ky < s.k; ++ky)
+          for (int kx = 0; kx < s.k; ++kx)
+            w[(((size_t)co * s.k + ky) * s.k + kx) * s.cin + c] =
+                (double)W[(((size_t)co * s.cin + c) * s.k + ky) * s.k + kx] * sc[co];
+    DevConv d;
+    d.spec = s;
+    if ((rc = upload_typed(&d.w, w, dtype))) return rc;
+    std::vector<float> bf(sh.begin(), sh.end());
+    if ((rc = upload((void**)&d.bias, bf))) return rc;
+    p->convs.push_back(d);
+  }
+  *out = p;
+  return SAD_OK;
+}
+
+extern "C" int sad_backbone_plan_destroy(sad_backbone_plan* p) {
+  if (!p) return SAD_OK;
+  (void)hipFree(p->stem_w);
+  (void)hipFree(p->stem_b);
+  for (auto& c : p->convs) {
+    (void)hipFree(c.w);
+    (void)hipFree(c.bias);
+  }
+  delete p;
+  return SAD_OK;
+}
+
+static constexpr int64_t kMaxActElems = 128ll * 128 * 64;  // per segment, layer1 map
+static size_t act_bytes(const sad_backbone_plan* p, int64_t mb) {
+  const size_t es = p->dtype == SAD_BF16 ? 2 : 4;
+  return ((size_t)mb * kMaxActElems * es + 255) & ~(size_t)255;
+}
+
+extern "C" int sad_backbone_workspace_size(const sad_backbone_plan* p, int64_t mb, size_t* bytes) {
+  SAD_REQUIRE(p && bytes && mb > 0, "bad args");
+  *bytes = 4 * act_bytes(p, mb);
+  return SAD_OK;
+}
+
+static int run_chunk(const sad_backbone_plan* p, const float* map, int64_t mb, float* feats,
+                     void* layer4_out, char* ws, hipStream_t s) {
+  const size_t ab = act_bytes(p, mb);
+  void* bufA = ws;
+  void* bufB = ws + ab;
+  void* bufT = ws + 2 * ab;
+  void* bufD = ws + 3 * ab;
+  StemArgs st{map, p->mh, p->mw, p->stem_w, p->stem_b, bufA, mb};
+  int rc = launch_stem(st, p->dtype, s);
+  if (rc) return rc;
+  int H = 128, C = 64;
+  size_t ci = 0;
+  for (int li = 0; li < 4; ++li) {
+    for (int b = 0; b < 2; ++b) {
+      const DevConv& c1 = p->convs[ci++];
+      const DevConv& c2 = p->convs[ci++];
+      const DevConv* ds = nullptr;
+      if (b == 0 && li > 0) ds = &p->convs[ci++];
+      const int Ho = H / c1.spec.stride;
+      ConvArgs a{};
+      a.in = bufA;
+      a.in_pstride = C;
+      a.N = (int)mb;
+      a.H = H;
+      a.W = H;
+      a.Cin = C;
+      a.wt = c1.w;
+      a.bias = c1.bias;
+      a.res = nullptr;
+      a.out = bufT;
+      a.out_pstride = c1.spec.cout;
+      a.Ho = Ho;
+      a.Wo = Ho;
+      a.Cout = c1.spec.cout;
+      a.KH = a.KW = c1.spec.k;
+      a.stride = c1.spec.stride;
+      a.pad = c1.spec.pad;
+      a.relu = 1;
+      a.M = mb * Ho * Ho;
+      if ((rc = launch_conv(a, p->dtype, s))) return rc;
+      const void* res = bufA;
+      if (ds) {
+        ConvArgs d = a;
+        d.wt = ds->w;
+        d.bias = ds->bias;
+        d.out = bufD;
+        d.KH = d.KW = 1;
+        d.pad = 0;
+        d.relu = 0;
+        if ((rc = launch_conv(d, p->dtype, s))) return rc;
+        res = bufD;
+      }
+      ConvArgs a2{};
+      a2.in = bufT;
+      a2.in_pstride = c2.spec.cin;
+      a2.N = (int)mb;
+      a2.H = Ho;
+      a2.W = Ho;
+      a2.Cin = c2.spec.cin;
+      a2.wt = c2.w;
+      a2.bias = c2.bias;
+      a2.res = res;
+      a2.res_pstride = c2.spec.cout;
+      a2.out = bufB;
+      a2.out_pstride = c2.spec.cout;
+      a2.Ho = Ho;
+      a2.Wo = Ho;
+      a2.Cout = c2.spec.cout;
+      a2.KH = a2.KW = 3;
+      a2.stride = 1;
+      a2.pad = 1;
+      a2.relu = 1;
+      a2.M = mb * Ho * Ho;
+      if ((rc = launch_conv(a2, p->dtype, s))) return rc;
+      std::swap(bufA, bufB);
+      H = Ho;
+      C = c2.spec.cout;
+    }
+  }
+  if (layer4_out) {
+    const size_t es = p->dtype == SAD_BF16 ? 2 : 4;
+    SAD_CHECK_HIP(hipMemcpyAsync(layer4_out, bufA, (size_t)mb * H * H * C * es, hipMemcpyDeviceToDevice, s));
+  }
+  return launch_avgpool(bufA, mb, H * H, C, feats, p->dtype, s);
+}
+
+extern "C" int sad_backbone_run(const sad_backbone_plan* p, const float* map, int64_t B, int64_t mb,
+                                float* feats, void* ws, size_t ws_bytes, void* stream) {
+  SAD_REQUIRE(p && feats && ws, "null args");
+  SAD_REQUIRE(B >= 0 && mb > 0, "bad batch");
+  size_t need = 0;
+  sad_backbone_workspace_size(p, mb, &need);
+  if (ws_bytes < need) {
+    set_error("workspace too small");
+    return SAD_ERR_NOMEM;
+  }
+  const int64_t plane = (int64_t)p->mh * p->mw;
+  for (int64_t i = 0; i < B; i += mb) {
+    const int64_t n = std::min(mb, B - i);
+    int rc = run_chunk(p, map + i * plane, n, feats + i * 512, nullptr, (char*)ws, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return SAD_OK;
+}
+
+extern "C" int sad_backbone_run_debug(const sad_backbone_plan* p, const float* map, int64_t B, float* feats,
+                                      void* layer4_out, void* ws, size_t ws_bytes, void* stream) {
+  SAD_REQUIRE(p && feats && ws && layer4_out && B > 0, "null args");
+  size_t need = 0;
+  sad_backbone_workspace_size(p, B, &need);
+  if (ws_bytes < need) {
+    set_error("workspace too small (debug run needs micro_batch = B)");
+    return SAD_ERR_NOMEM;
+  }
+  return run_chunk(p, map, B, feats, layer4_out, (char*)ws, (hipStream_t)stream);
+}
+
+extern "C" int sad_backbone_stem_run(const sad_backbone_plan* p, const float* map, int64_t B, void* out,
+                                     void* stream) {
+  SAD_REQUIRE(p && map && out && B >= 0, "null args");
+  StemArgs st{map, p->mh, p->mw, p->stem_w, p->stem_b, out, B};
+  return launch_stem(st, p->dtype, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------- heads ----
+extern "C" int sad_heads_plan_create(const float* const* params, int32_t n_heads, const int32_t* feat_index,
+                                     int32_t n_feat, sad_heads_plan** out) {
+  SAD_REQUIRE(params && out && n_heads > 0 && n_feat > 0, "bad args");
+  for (int i = 0; i < n_heads * 14; ++i) SAD_REQUIRE(params[i], "null head parameter");
+  auto* p = new sad_heads_plan();
+  p->n_heads = n_heads;
+  p->n_feat = n_feat;
+  (void)hipGetDevice(&p->device);
+  p->groups.assign(n_feat, {});
+  for (int h = 0; h < n_heads; ++h) {
+    const int f = feat_index ? feat_index[h] : 0;
+    SAD_REQUIRE(f >= 0 && f < n_feat, "feat_index out of range");
+    p->feat_index.push_back(f);
+    p->groups[f].push_back(h);
+  }
+  p->y1_col.assign(n_heads, 0);
+  int col = 0, rc;
+  std::vector<double> sc, sh;
+  for (int f = 0; f < n_feat; ++f) {
+    const auto& g = p->groups[f];
+    std::vector<float> w1((size_t)g.size() * 512 * 512), b1(g.size() * 512);
+    for (size_t gi = 0; gi < g.size(); ++gi) {
+      const float* const* hp = params + g[gi] * 14;
+      fold_bn(hp[2], hp[3], hp[4], hp[5], 512, sc, sh);
+      for (int o = 0; o < 512; ++o) {
+        for (int i = 0; i < 512; ++i) w1[(gi * 512 + o) * 512 + i] = (float)((double)hp[0][o * 512 + i] * sc[o]);
+        b1[gi * 512 + o] = (float)((double)hp[1][o] * sc[o] + sh[o]);
+      }
+      p->y1_col[g[gi]] = col;
+      col += 512;
+    }
+    void* dw = nullptr;
+    void* db = nullptr;
+    if (!g.empty()) {
+      if ((rc = upload(&dw, w1))) return rc;
+      if ((rc = upload(&db, b1))) return rc;
+    }
+    p->w1.push_back((float*)dw);
+    p->b1.push_back((float*)db);
+  }
+  std::vector<float> w2((size_t)n_heads * 256 * 512), b2(n_heads * 256), w3(n_heads * 512), b3(n_heads * 2);
+  for (int h = 0; h < n_heads; ++h) {
+    const float* const* hp = params + h * 14;
+    fold_bn(hp[8], hp[9], hp[10], hp[11], 256, sc, sh);
+    for (int o = 0; o < 256; ++o) {
+      for (int i = 0; i < 512; ++i) w2[((size_t)h * 256 + o) * 512 + i] = (float)((double)hp[6][o * 512 + i] * sc[o]);
+      b2[h * 256 + o] = (float)((double)hp[7][o] * sc[o] + sh[o]);
+    }
+    memcpy(&w3[h * 512], hp[12], 512 * sizeof(float));
+    memcpy(&b3[h * 2], hp[13], 2 * sizeof(float));
+  }
+  if ((rc = upload((void**)&p->w2, w2))) return rc;
+  if ((rc = upload((void**)&p->b2, b2))) return rc;
+  if ((rc = upload((void**)&p->w3, w3))) return rc;
+  if ((rc = upload((void**)&p->b3, b3))) return rc;
+  *out = p;
+  return SAD_OK;
+}
+
+extern "C" int sad_heads_plan_destroy(sad_heads_plan* p) {
+  if (!p) return SAD_OK;
+  for (auto* w : p->w1) (void)hipFree(w);
+  for (auto* b : p->b1) (void)hipFree(b);
+  (void)hipFree(p->w2);
+  (void)hipFree(p->b2);
+  (void)hipFree(p->w3);
+  (void)hipFree(p->b3);
+  delete p;
+  return SAD_OK;
+}
+
+extern "C" int sad_heads_workspace_size(const sad_heads_plan* p, int64_t B, size_t* bytes) {
+  SAD_REQUIRE(p && bytes && B >= 0, "bad args");
+  *bytes = (size_t)B * p->n_heads * (512 + 256) * sizeof(float) + 256;
+  return SAD_OK;
+}
+
+extern "C" int sad_heads_merge_run(const sad_heads_plan* p, const float* const* feats, int64_t B, float* logits,
+                                   float* merged, void* ws, size_t ws_bytes, void* stream) {
+  SAD_REQUIRE(p && feats && merged && ws, "null args");
+  size_t need = 0;
+  sad_heads_workspace_size(p, B, &need);
+  if (ws_bytes < need) {
+    set_error("heads workspace too small");
+    return SAD_ERR_NOMEM;
+  }
+  if (B == 0) return SAD_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int N = p->n_heads;
+  float* y1 = (float*)ws;
+  float* y2 = y1 + (size_t)B * N * 512;
+  int rc, col = 0;
+  for (int f = 0; f < p->n_feat; ++f) {
+    const int G = (int)p->groups[f].size();
+    if (!G) continue;
+    SAD_REQUIRE(feats[f], "null feature pointer");
+    ConvArgs a{};
+    a.in = feats[f];
+    a.in_pstride = 512;
+    a.N = (int)B;
+    a.H = a.W = 1;
+    a.Cin = 512;
+    a.wt = p->w1[f];
+    a.bias = p->b1[f];
+    a.out = y1 + col;
+    a.out_pstride = (int64_t)N * 512;
+    a.Ho = a.Wo = 1;
+    a.Cout = 512 * G;
+    a.KH = a.KW = 1;
+    a.stride = 1;
+    a.pad = 0;
+    a.relu = 1;
+    a.M = B;
+    if ((rc = launch_conv(a, SAD_F32, s))) return rc;
+    col += 512 * G;
+  }
+  for (int h = 0; h < N; ++h) {
+    ConvArgs a{};
+    a.in = y1 + p->y1_col[h];
+    a.in_pstride = (int64_t)N * 512;
+    a.N = (int)B;
+    a.H = a.W = 1;
+    a.Cin = 512;
+    a.wt = p->w2 + (size_t)h * 256 * 512;
+    a.bias = p->b2 + h * 256;
+    a.out = y2 + h * 256;
+    a.out_pstride = (int64_t)N * 256;
+    a.Ho = a.Wo = 1;
+    a.Cout = 256;
+    a.KH = a.KW = 1;
+    a.stride = 1;
+    a.pad = 0;
+    a.relu = 1;
+    a.M = B;
+    if ((rc = launch_conv(a, SAD_F32, s))) return rc;
+  }
+  return launch_heads_final(y2, B, N, p->w3, p->b3, logits, merged, s);
+}

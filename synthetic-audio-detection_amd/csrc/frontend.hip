@@ -1,0 +1,390 @@
+// frontend.hip -- fused int16 PCM -> Hann -> rFFT(2048) -> |X|^2 -> mel -> dB
+// -> per-segment top-db clamp + standardisation, for gfx950.
+//
+// Replaces torchaudio MelSpectrogram + AmplitudeToDB + the (x-mean)/(std+1e-6)
+// step of inference_runner.py:157-171 (semantics: SURVEY.md Appendix A).
+//
+// Kernel 1 (fe_mel_db): one workgroup = 4 waves = one segment x a block of 32
+//   STFT frames; each wave owns one frame at a time.  A 2048-point real frame
+//   is packed as a 1024-point complex sequence z[m] = y[2m] + i*y[2m+1] and
+//   transformed by a 5-pass radix-4 Stockham FFT whose butterflies run in
+//   registers and whose passes exchange through the wave's 8 KB LDS slot;
+//   twiddles (1024- and 2048-point, float64-accurate) live in LDS.  The real
+//   spectrum is recovered for the bins the mel bank touches (2..768), powered,
+//   projected on the CSR mel bank (1515 nnz) and converted to dB.
+//   PCM reads: the first Stockham pass loads z straight from HBM, lane-
+//   consecutive int16 pairs (coalesced); reflect padding is index arithmetic.
+// Kernel 2 (fe_normalize): one workgroup per segment: max -> top-db clamp ->
+//   float64 mean / unbiased variance -> standardise (32,128 values).
+#include <math.h>
+
+#include <vector>
+
+#include "common.hpp"
+
+namespace sad {
+
+constexpr int FE_NFFT = 2048;
+constexpr int FE_NC = 1024;         // complex FFT length
+constexpr int FE_FRAMES_PER_WG = 32;
+constexpr int FE_WAVES = 4;
+
+struct FrontendPlan {
+  sad_frontend_cfg cfg;
+  int n_frames;
+  int bin_lo, bin_hi;         // mel bank nonzero bin range [lo, hi]
+  float2* d_tw1024 = nullptr;  // e^{-2 pi i m / 1024}, m < 1024
+  float2* d_tw2048 = nullptr;  // e^{-2 pi i k / 2048}, k <= 1024
+  float* d_window = nullptr;   // periodic Hann(2048)
+  int* d_mel_start = nullptr;  // [n_mels] first bin
+  int* d_mel_len = nullptr;    // [n_mels]
+  int* d_mel_off = nullptr;    // [n_mels] offset into d_mel_w
+  float* d_mel_w = nullptr;    // packed nonzero weights
+  int device = 0;
+};
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+__global__ __launch_bounds__(256) void fe_mel_db_kernel(
+    const int16_t* __restrict__ pcm, int64_t seg_stride, int n_samples, int n_frames, int hop,
+    const float2* __restrict__ tw1024, const float2* __restrict__ tw2048,
+    const float* __restrict__ window, const int* __restrict__ mel_start,
+    const int* __restrict__ mel_len, const int* __restrict__ mel_off,
+    const float* __restrict__ mel_w, int n_mels, int bin_lo, int bin_hi, float* __restrict__ out) {
+  __shared__ float2 s_tw[FE_NC];
+  __shared__ float2 s_tw2[FE_NC + 1];
+  __shared__ float2 s_buf[FE_WAVES][FE_NC];
+  __shared__ float s_pow[FE_WAVES][FE_NC];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t seg = blockIdx.y;
+  const int16_t* x = pcm + seg * seg_stride;
+  for (int i = tid; i < FE_NC; i += 256) s_tw[i] = tw1024[i];
+  for (int i = tid; i <= FE_NC; i += 256) s_tw2[i] = tw2048[i];
+  __syncthreads();
+
+  const int f_begin = blockIdx.x * FE_FRAMES_PER_WG;
+  const int f_end = min(n_frames, f_begin + FE_FRAMES_PER_WG);
+  float2* buf = s_buf[wave];
+  float* pw = s_pow[wave];
+  const int pad = FE_NFFT / 2;
+
+  for (int f0 = f_begin; f0 < f_end; f0 += FE_WAVES) {
+    const int t = f0 + wave;
+    const bool active = t < f_end;  // wave-uniform
+    float2 v[4][4];
+    // ---- pass 0 (Ns = 1): load z[j + 256 r] straight from global
+    if (active) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int j = lane + 64 * b;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = j + 256 * r;
+          float e[2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int n = 2 * m + q;
+            int idx = t * hop + n - pad;
+            idx = idx < 0 ? -idx : idx;
+            idx = idx >= n_samples ? 2 * (n_samples - 1) - idx : idx;
+            e[q] = (float)x[idx] * (1.0f / 32768.0f) * window[n];
+          }
+          v[b][r] = make_float2(e[0], e[1]);
+        }
+      }
+    }
+    // ---- 5 radix-4 Stockham passes, Ns = 1, 4, 16, 64, 256
+#pragma unroll
+    for (int p = 0; p < 5; ++p) {
+      const int Ns = 1 << (2 * p);
+      if (active) {
+        if (p > 0) {
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int j = lane + 64 * b;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[b][r] = buf[j + 256 * r];
+          }
+        }
+      }
+      __syncthreads();
+      if (active) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int j = lane + 64 * b;
+          const int k = j & (Ns - 1);
+          if (p > 0) {
+            const int tstep = FE_NC / (Ns * 4);  // angle index step per r
+#pragma unroll
+            for (int r = 1; r < 4; ++r) v[b][r] = cmul(v[b][r], s_tw[(k * r * tstep) & (FE_NC - 1)]);
+          }
+          // radix-4 forward DFT
+          const float2 a0 = v[b][0], a1 = v[b][1], a2 = v[b][2], a3 = v[b][3];
+          const float2 s02 = make_float2(a0.x + a2.x, a0.y + a2.y);
+          const float2 d02 = make_float2(a0.x - a2.x, a0.y - a2.y);
+          const float2 s13 = make_float2(a1.x + a3.x, a1.y + a3.y);
+          const float2 d13 = make_float2(a1.x - a3.x, a1.y - a3.y);
+          const int idxD = (j / Ns) * Ns * 4 + k;
+          buf[idxD] = make_float2(s02.x + s13.x, s02.y + s13.y);
+          buf[idxD + Ns] = make_float2(d02.x + d13.y, d02.y - d13.x);      // a0 - i a1 - a2 + i a3
+          buf[idxD + 2 * Ns] = make_float2(s02.x - s13.x, s02.y - s13.y);
+          buf[idxD + 3 * Ns] = make_float2(d02.x - d13.y, d02.y + d13.x);  // a0 + i a1 - a2 - i a3
+        }
+      }
+      __syncthreads();
+    }
+    // ---- real-spectrum recovery + power for bins [bin_lo, bin_hi]
+    if (active) {
+      for (int k = bin_lo + lane; k <= bin_hi; k += 64) {
+        const float2 A = buf[k & (FE_NC - 1)];
+        const float2 Bc = buf[(FE_NC - k) & (FE_NC - 1)];
+        const float2 B = make_float2(Bc.x, -Bc.y);              // conj(Z[N/2-k])
+        const float2 E = make_float2(0.5f * (A.x + B.x), 0.5f * (A.y + B.y));
+        const float2 D = make_float2(A.x - B.x, A.y - B.y);
+        const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);  // -i/2 (A - B)
+        const float2 WO = cmul(s_tw2[k], O);
+        const float re = E.x + WO.x, im = E.y + WO.y;
+        pw[k - bin_lo] = re * re + im * im;
+      }
+    }
+    __syncthreads();
+    if (active) {
+      for (int m = lane; m < n_mels; m += 64) {
+        const int k0 = mel_start[m], len = mel_len[m], off = mel_off[m];
+        float acc = 0.f;
+        for (int q = 0; q < len; ++q) acc = fmaf(pw[k0 + q - bin_lo], mel_w[off + q], acc);
+        const float db = 10.0f * log10f(fmaxf(acc, 1e-10f));
+        out[(seg * n_mels + m) * n_frames + t] = db;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+__global__ __launch_bounds__(1024) void fe_normalize_kernel(float* db_io, int count,
+                                                             float top_db, float* map_out) {
+  __shared__ double red[16];
+  __shared__ float redf[16];
+  const int64_t seg = blockIdx.x;
+  float* x = db_io + seg * count;
+  float* y = map_out + seg * count;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float mx = -INFINITY;
+  for (int i = tid; i < count; i += blockDim.x) mx = fmaxf(mx, x[i]);
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if (lane == 0) redf[wave] = mx;
+  __syncthreads();
+  mx = redf[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) mx = fmaxf(mx, redf[i]);
+  const float floor_db = top_db >= 0.f ? mx - top_db : -INFINITY;
+  double s = 0.0;
+  for (int i = tid; i < count; i += blockDim.x) {
+    float v = fmaxf(x[i], floor_db);
+    if (x != y) x[i] = v;  // caller asked for the clamped dB map
+    s += (double)v;
+  }
+  const double mean = block_sum_d(s, red) / count;
+  const float mean_f = (float)mean;
+  double ss = 0.0;
+  for (int i = tid; i < count; i += blockDim.x) {
+    const double d = (double)fmaxf(x[i], floor_db) - mean;
+    ss += d * d;
+  }
+  const double var = block_sum_d(ss, red) / (count - 1);
+  const float denom = (float)sqrt(var) + 1e-6f;
+  for (int i = tid; i < count; i += blockDim.x) {
+    const float v = fmaxf(x[i], floor_db);
+    y[i] = (v - mean_f) / denom;
+  }
+}
+
+// Bilinear resize, align_corners=False (torchvision Resize on tensors; antialias
+// is a no-op for upsampling).  One thread per output pixel.
+template <typename OT>
+__global__ void resize_kernel(const float* __restrict__ in, int h, int w, int oh, int ow,
+                              OT* __restrict__ out, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int ox = i % ow;
+  const int oy = (i / ow) % oh;
+  const int64_t n = i / ((int64_t)ow * oh);
+  const float sh = (float)h / oh, sw = (float)w / ow;
+  float fy = sh * (oy + 0.5f) - 0.5f;
+  fy = fy < 0.f ? 0.f : fy;
+  float fx = sw * (ox + 0.5f) - 0.5f;
+  fx = fx < 0.f ? 0.f : fx;
+  const int y0 = min((int)floorf(fy), h - 1), x0 = min((int)floorf(fx), w - 1);
+  const int y1 = min(y0 + 1, h - 1), x1 = min(x0 + 1, w - 1);
+  const float ly = fminf(fmaxf(fy - y0, 0.f), 1.f), lx = fminf(fmaxf(fx - x0, 0.f), 1.f);
+  const float* p = in + n * h * w;
+  const float v = (1.f - ly) * ((1.f - lx) * p[y0 * w + x0] + lx * p[y0 * w + x1]) +
+                  ly * ((1.f - lx) * p[y1 * w + x0] + lx * p[y1 * w + x1]);
+  if constexpr (sizeof(OT) == 2)
+    out[i] = f2bf(v);
+  else
+    out[i] = v;
+}
+
+// ---- host: mel filterbank (torchaudio melscale_fbanks, htk), float64 then f32
+static std::vector<float> mel_fbank(int n_freqs, double f_min, double f_max, int n_mels, int sr, bool slaney) {
+  auto hz2mel = [](double f) { return 2595.0 * log10(1.0 + f / 700.0); };
+  auto mel2hz = [](double m) { return 700.0 * (pow(10.0, m / 2595.0) - 1.0); };
+  std::vector<double> fpts(n_mels + 2);
+  const double mmin = hz2mel(f_min), mmax = hz2mel(f_max);
+  for (int i = 0; i < n_mels + 2; ++i) fpts[i] = mel2hz(mmin + (mmax - mmin) * i / (n_mels + 1));
+  std::vector<float> fb((size_t)n_freqs * n_mels, 0.f);
+  for (int k = 0; k < n_freqs; ++k) {
+    const double f = (double)(sr / 2) * k / (n_freqs - 1);
+    for (int m = 0; m < n_mels; ++m) {
+      const double down = (f - fpts[m]) / (fpts[m + 1] - fpts[m]);
+      const double up = (fpts[m + 2] - f) / (fpts[m + 2] - fpts[m + 1]);
+      double v = fmax(0.0, fmin(down, up));
+      if (slaney) v *= 2.0 / (fpts[m + 2] - fpts[m]);
+      fb[(size_t)k * n_mels + m] = (float)v;
+    }
+  }
+  return fb;
+}
+
+}  // namespace sad
+
+using namespace sad;
+
+struct sad_frontend_plan : sad::FrontendPlan {};
+
+extern "C" int sad_frontend_plan_create(const sad_frontend_cfg* cfg, sad_frontend_plan** out) {
+  SAD_REQUIRE(cfg && out, "null cfg/out");
+  SAD_REQUIRE(cfg->n_fft == FE_NFFT, "only n_fft = 2048 is supported");
+  SAD_REQUIRE(cfg->hop_length > 0 && cfg->n_mels > 0 && cfg->n_mels <= 1024, "hop/n_mels");
+  SAD_REQUIRE(cfg->n_samples > FE_NFFT / 2, "n_samples must exceed n_fft/2 (reflect pad)");
+  auto* p = new sad_frontend_plan();
+  p->cfg = *cfg;
+  p->n_frames = 1 + cfg->n_samples / cfg->hop_length;
+  (void)hipGetDevice(&p->device);
+  const int n_freqs = FE_NFFT / 2 + 1;
+  std::vector<float> fb = mel_fbank(n_freqs, cfg->f_min, cfg->f_max, cfg->n_mels, cfg->sample_rate,
+                                    cfg->norm_slaney != 0);
+  std::vector<int> st(cfg->n_mels), ln(cfg->n_mels), off(cfg->n_mels);
+  std::vector<float> w;
+  int lo = n_freqs, hi = -1;
+  for (int m = 0; m < cfg->n_mels; ++m) {
+    int a = -1, b = -1;
+    for (int k = 0; k < n_freqs; ++k)
+      if (fb[(size_t)k * cfg->n_mels + m] != 0.f) {
+        if (a < 0) a = k;
+        b = k;
+      }
+    if (a < 0) a = b = 0;  // empty filter: contributes 0 (weight 0 at bin 0)
+    st[m] = a;
+    ln[m] = b - a + 1;
+    off[m] = (int)w.size();
+    for (int k = a; k <= b; ++k) w.push_back(fb[(size_t)k * cfg->n_mels + m]);
+    lo = std::min(lo, a);
+    hi = std::max(hi, b);
+  }
+  p->bin_lo = lo;
+  p->bin_hi = hi;
+  std::vector<float2> tw(FE_NC), tw2(FE_NC + 1);
+  for (int m = 0; m < FE_NC; ++m) {
+    const double a = -2.0 * M_PI * m / FE_NC;
+    tw[m] = make_float2((float)cos(a), (float)sin(a));
+  }
+  for (int k = 0; k <= FE_NC; ++k) {
+    const double a = -2.0 * M_PI * k / FE_NFFT;
+    tw2[k] = make_float2((float)cos(a), (float)sin(a));
+  }
+  std::vector<float> win(FE_NFFT);
+  for (int n = 0; n < FE_NFFT; ++n) win[n] = (float)(0.5 - 0.5 * cos(2.0 * M_PI * n / FE_NFFT));
+#define UP(dst, vec)                                                                   \
+  SAD_CHECK_HIP(hipMalloc((void**)&dst, vec.size() * sizeof(vec[0])));                 \
+  SAD_CHECK_HIP(hipMemcpy(dst, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice));
+  UP(p->d_tw1024, tw);
+  UP(p->d_tw2048, tw2);
+  UP(p->d_window, win);
+  UP(p->d_mel_start, st);
+  UP(p->d_mel_len, ln);
+  UP(p->d_mel_off, off);
+  UP(p->d_mel_w, w);
+#undef UP
+  *out = p;
+  return SAD_OK;
+}
+
+extern "C" int sad_frontend_plan_destroy(sad_frontend_plan* p) {
+  if (!p) return SAD_OK;
+  (void)hipFree(p->d_tw1024);
+  (void)hipFree(p->d_tw2048);
+  (void)hipFree(p->d_window);
+  (void)hipFree(p->d_mel_start);
+  (void)hipFree(p->d_mel_len);
+  (void)hipFree(p->d_mel_off);
+  (void)hipFree(p->d_mel_w);
+  delete p;
+  return SAD_OK;
+}
+
+extern "C" int sad_frontend_frames(const sad_frontend_plan* p, int32_t* n) {
+  SAD_REQUIRE(p && n, "null");
+  *n = p->n_frames;
+  return SAD_OK;
+}
+
+extern "C" int sad_frontend_run(const sad_frontend_plan* p, const int16_t* pcm, int64_t n_seg,
+                                int64_t seg_stride, float* out_db, float* out_map, void* stream) {
+  SAD_REQUIRE(p, "null plan");
+  SAD_REQUIRE(n_seg >= 0 && n_seg < 65536 * 32, "n_seg out of range");
+  SAD_REQUIRE(out_map, "out_map is required");
+  SAD_REQUIRE(seg_stride >= p->cfg.n_samples, "seg_stride < n_samples");
+  if (n_seg == 0) return SAD_OK;
+  SAD_REQUIRE(pcm, "null pcm");
+  hipStream_t s = (hipStream_t)stream;
+  float* dbbuf = out_db ? out_db : out_map;
+  const int n_fb = (p->n_frames + FE_FRAMES_PER_WG - 1) / FE_FRAMES_PER_WG;
+  int64_t done = 0;
+  while (done < n_seg) {  // gridDim.y <= 65535
+    const int64_t chunk = std::min<int64_t>(65535, n_seg - done);
+    const size_t off = (size_t)done * p->cfg.n_mels * p->n_frames;
+    hipLaunchKernelGGL(fe_mel_db_kernel, dim3(n_fb, (unsigned)chunk), dim3(256), 0, s,
+                       pcm + done * seg_stride, seg_stride, p->cfg.n_samples, p->n_frames,
+                       p->cfg.hop_length, p->d_tw1024, p->d_tw2048, p->d_window, p->d_mel_start,
+                       p->d_mel_len, p->d_mel_off, p->d_mel_w, p->cfg.n_mels, p->bin_lo, p->bin_hi,
+                       dbbuf + off);
+    SAD_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(fe_normalize_kernel, dim3((unsigned)chunk), dim3(1024), 0, s, dbbuf + off,
+                       p->cfg.n_mels * p->n_frames, p->cfg.top_db, out_map + off);
+    SAD_CHECK_HIP(hipGetLastError());
+    done += chunk;
+  }
+  return SAD_OK;
+}
+
+extern "C" int sad_resize_run(const float* map, int64_t n, int32_t h, int32_t w, int32_t oh,
+                              int32_t ow, int32_t dtype, void* img, void* stream) {
+  SAD_REQUIRE(h > 0 && w > 0 && oh > 0 && ow > 0 && n >= 0, "bad shape");
+  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
+  const int64_t total = n * oh * ow;
+  if (total == 0) return SAD_OK;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  if (dtype == SAD_F32)
+    hipLaunchKernelGGL(resize_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, map, h, w,
+                       oh, ow, (float*)img, total);
+  else
+    hipLaunchKernelGGL(resize_kernel<u16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, map, h, w,
+                       oh, ow, (u16*)img, total);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
+}

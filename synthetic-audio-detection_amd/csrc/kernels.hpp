@@ -1,0 +1,38 @@
+// kernels.hpp -- launch interfaces shared by the kernel translation units.
+#pragma once
+#include "common.hpp"
+
+namespace sad {
+
+struct ConvArgs {
+  const void* in;        // NHWC [N, H, W, *] with pixel stride in_pstride (elements)
+  int64_t in_pstride;
+  int N, H, W, Cin;
+  const void* wt;        // [Cout][KH][KW][Cin], BN folded
+  const float* bias;     // [Cout], BN folded
+  const void* res;       // optional residual, [M, *] pixel stride res_pstride
+  int64_t res_pstride;
+  void* out;             // [M, *] pixel stride out_pstride
+  int64_t out_pstride;
+  int Ho, Wo, Cout, KH, KW, stride, pad;
+  int relu;
+  int64_t M;             // N * Ho * Wo
+};
+
+struct StemArgs {
+  const float* map;      // [B, mh, mw] standardised maps
+  int mh, mw;
+  const void* w;         // [64 co][64 k] folded conv1 (k = ky*7+kx, zero for k >= 49),
+                         // f32 variant permuted: position g*16+q holds k = 4q+g
+  const float* bias;     // [64]
+  void* out;             // NHWC [B, 128, 128, 64]
+  int64_t B;
+};
+
+int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
+int launch_stem(const StemArgs& a, int dtype, hipStream_t s);
+int launch_avgpool(const void* in, int64_t B, int hw, int c, float* out, int dtype, hipStream_t s);
+int launch_heads_final(const float* y2, int64_t B, int n_heads, const float* w3, const float* b3,
+                       float* logits, float* merged, hipStream_t s);
+
+}  // namespace sad

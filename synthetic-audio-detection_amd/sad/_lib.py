@@ -1,0 +1,100 @@
+"""ctypes binding of libsad.so (include/sad.h).
+
+torch is imported first on purpose: torch ships its own ``libamdhip64.so.7``;
+loading it before libsad makes the dynamic linker resolve libsad's
+``libamdhip64.so.7`` dependency to the SAME runtime instance, so torch's device
+pointers and streams are valid inside libsad.
+
+There is no fallback: if the library is missing or fails to load, every entry
+point raises.  (The product path never routes to a CPU implementation.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('SAD_LIB', os.path.join(_HERE, 'libsad.so'))
+
+SAD_F32 = 0
+SAD_BF16 = 1
+
+# name -> (restype, argtypes); exactly the symbols include/sad.h declares.
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+SZ = ctypes.c_size_t
+FPP = ctypes.POINTER(ctypes.c_void_p)
+
+
+class FrontendCfg(ctypes.Structure):
+    _fields_ = [('sample_rate', I32), ('n_fft', I32), ('hop_length', I32), ('n_mels', I32),
+                ('f_min', ctypes.c_float), ('f_max', ctypes.c_float), ('norm_slaney', I32),
+                ('top_db', ctypes.c_float), ('n_samples', I32)]
+
+
+SIGNATURES = {
+    'sad_init': (ctypes.c_int, [ctypes.c_int]),
+    'sad_last_error': (ctypes.c_char_p, []),
+    'sad_version': (ctypes.c_char_p, []),
+    'sad_frontend_plan_create': (ctypes.c_int, [ctypes.POINTER(FrontendCfg), ctypes.POINTER(P)]),
+    'sad_frontend_plan_destroy': (ctypes.c_int, [P]),
+    'sad_frontend_frames': (ctypes.c_int, [P, ctypes.POINTER(I32)]),
+    'sad_frontend_run': (ctypes.c_int, [P, P, I64, I64, P, P, P]),
+    'sad_resize_run': (ctypes.c_int, [P, I64, I32, I32, I32, I32, I32, P, P]),
+    'sad_backbone_plan_create': (ctypes.c_int, [FPP, I32, I32, I32, I32, ctypes.POINTER(P)]),
+    'sad_backbone_plan_destroy': (ctypes.c_int, [P]),
+    'sad_backbone_workspace_size': (ctypes.c_int, [P, I64, ctypes.POINTER(SZ)]),
+    'sad_backbone_run': (ctypes.c_int, [P, P, I64, I64, P, P, SZ, P]),
+    'sad_backbone_stem_run': (ctypes.c_int, [P, P, I64, P, P]),
+    'sad_backbone_run_debug': (ctypes.c_int, [P, P, I64, P, P, P, SZ, P]),
+    'sad_heads_plan_create': (ctypes.c_int, [FPP, I32, ctypes.POINTER(I32), I32, ctypes.POINTER(P)]),
+    'sad_heads_plan_destroy': (ctypes.c_int, [P]),
+    'sad_heads_workspace_size': (ctypes.c_int, [P, I64, ctypes.POINTER(SZ)]),
+    'sad_heads_merge_run': (ctypes.c_int, [P, FPP, I64, P, P, P, SZ, P]),
+    'sad_synth_pcm': (ctypes.c_int, [ctypes.c_uint64, I64, I64, I32, P, P]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libsad.so (once) and attach prototypes; raises if unavailable."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f'libsad.so not found at {LIB_PATH}; build it with '
+                               f'`python -c "import __graft_entry__ as g; g.build()"`')
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str = ''):
+    if rc != 0:
+        msg = load().sad_last_error().decode(errors='replace')
+        raise RuntimeError(f'libsad {what} failed ({rc}): {msg}')
+
+
+def call(name: str, *args):
+    check(getattr(load(), name)(*args), name)
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def pointer_array(arrays):
+    """Keep-alive list + C array of host pointers to contiguous fp32 numpy arrays."""
+    arr = (ctypes.c_void_p * len(arrays))(*[a.ctypes.data for a in arrays])
+    return arr

@@ -1,0 +1,266 @@
+"""Device engine: front end, backbone(s) and heads as libsad plans.
+
+This is the MI355X replacement of the reference's device work:
+  * ``FrontEnd``  -- torchaudio MelSpectrogram/AmplitudeToDB + standardise
+    (inference_runner.py:157-171; trainer norm=None variant
+    submodel_trainer.py:97-105,191-199)
+  * ``Backbone``  -- timm resnet18 forward_features + AdaptiveAvgPool2d
+    (inference_runner.py:35,37,49-51), with Resize((512,512)) + repeat(3)
+    (:172-174) fused into the stem
+  * ``Heads``     -- BinaryClassifier.head x N + ModularMultiHeadClassifier
+    merge (inference_runner.py:36-48,62-73)
+  * ``Engine``    -- a merged checkpoint's state dict -> the three above.
+    Sub-models whose ``base.*`` tensors are identical (the reference's quirk
+    C2 makes that the normal case) share ONE backbone run.
+
+Every call is asynchronous on torch's current stream of the engine's device.
+"""
+from __future__ import annotations
+
+import hashlib
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .weights import backbone_param_shapes
+
+MAP_H, MAP_W = 128, 251
+N_SAMPLES = 128000
+HEAD_KEYS = ['2.weight', '2.bias', '3.weight', '3.bias', '3.running_mean', '3.running_var',
+             '6.weight', '6.bias', '7.weight', '7.bias', '7.running_mean', '7.running_var',
+             '10.weight', '10.bias']
+
+
+def _dev(device) -> torch.device:
+    d = torch.device(device)
+    if d.type != 'cuda':
+        raise RuntimeError(f'libsad runs on MI355X devices only (got {d}); there is no CPU path')
+    return torch.device('cuda', d.index if d.index is not None else torch.cuda.current_device())
+
+
+def _np32(t) -> np.ndarray:
+    return np.ascontiguousarray(torch.as_tensor(t).detach().to('cpu', torch.float32).numpy())
+
+
+class FrontEnd:
+    def __init__(self, device='cuda', norm: str | None = 'slaney', n_samples: int = N_SAMPLES,
+                 sample_rate: int = 32000, n_fft: int = 2048, hop: int = 512, n_mels: int = 128,
+                 f_min: float = 20.0, f_max: float = 12000.0, top_db: float | None = 80.0):
+        self.device = _dev(device)
+        cfg = _lib.FrontendCfg(sample_rate, n_fft, hop, n_mels, f_min, f_max, 1 if norm == 'slaney' else 0,
+                               -1.0 if top_db is None else float(top_db), n_samples)
+        self._plan = _lib.P()
+        with torch.cuda.device(self.device):
+            _lib.call('sad_frontend_plan_create', _lib.ctypes.byref(cfg), _lib.ctypes.byref(self._plan))
+        nf = _lib.I32()
+        _lib.call('sad_frontend_frames', self._plan, _lib.ctypes.byref(nf))
+        self.n_frames, self.n_mels, self.n_samples = nf.value, n_mels, n_samples
+
+    def __call__(self, pcm: torch.Tensor, want_db: bool = False):
+        """pcm [n, >=n_samples] int16 on device -> map [n, n_mels, frames] fp32
+        (and the clamped dB map if want_db)."""
+        assert pcm.dtype == torch.int16 and pcm.device == self.device and pcm.dim() == 2
+        assert pcm.stride(1) == 1 and pcm.shape[1] >= self.n_samples
+        n = pcm.shape[0]
+        out = torch.empty(n, self.n_mels, self.n_frames, device=self.device, dtype=torch.float32)
+        db = torch.empty_like(out) if want_db else None
+        with torch.cuda.device(self.device):
+            _lib.call('sad_frontend_run', self._plan, _lib.ptr(pcm), n, pcm.stride(0), _lib.ptr(db),
+                      _lib.ptr(out), _lib.stream_handle(self.device))
+        return (out, db) if want_db else out
+
+    def __del__(self):
+        try:
+            if getattr(self, '_plan', None):
+                _lib.load().sad_frontend_plan_destroy(self._plan)
+        except Exception:
+            pass
+
+
+def resize(map_: torch.Tensor, size=(512, 512), dtype: str = 'fp32') -> torch.Tensor:
+    """Device bilinear resize (torchvision Resize semantics) of [n, h, w] fp32."""
+    n, h, w = map_.shape
+    dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
+    out = torch.empty(n, size[0], size[1], device=map_.device,
+                      dtype=torch.bfloat16 if dt == _lib.SAD_BF16 else torch.float32)
+    with torch.cuda.device(map_.device):
+        _lib.call('sad_resize_run', _lib.ptr(map_.contiguous()), n, h, w, size[0], size[1], dt, _lib.ptr(out),
+                  _lib.stream_handle(map_.device))
+    return out
+
+
+class Backbone:
+    """One ResNet-18 backbone; ``base_sd`` uses timm keys (conv1.weight, ...)."""
+
+    def __init__(self, base_sd: Dict[str, torch.Tensor], device='cuda', dtype: str = 'bf16',
+                 micro_batch: int = 64):
+        self.device = _dev(device)
+        self.dtype = dtype
+        self._dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
+        self.tdtype = torch.bfloat16 if dtype == 'bf16' else torch.float32
+        self.micro_batch = micro_batch
+        arrays = []
+        for key, _shape, kind in backbone_param_shapes():
+            if kind == 'conv':
+                arrays.append(_np32(base_sd[f'{key}.weight']))
+            else:
+                for s in ('weight', 'bias', 'running_mean', 'running_var'):
+                    arrays.append(_np32(base_sd[f'{key}.{s}']))
+        self._keep = arrays
+        ptrs = _lib.pointer_array(arrays)
+        self._plan = _lib.P()
+        with torch.cuda.device(self.device):
+            _lib.call('sad_backbone_plan_create', ptrs, len(arrays), self._dt, MAP_H, MAP_W,
+                      _lib.ctypes.byref(self._plan))
+        self._ws = None
+
+    def workspace(self, mb: int) -> torch.Tensor:
+        sz = _lib.SZ()
+        _lib.call('sad_backbone_workspace_size', self._plan, mb, _lib.ctypes.byref(sz))
+        if self._ws is None or self._ws.numel() < sz.value:
+            self._ws = torch.empty(sz.value, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def __call__(self, maps: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        assert maps.dtype == torch.float32 and maps.shape[1:] == (MAP_H, MAP_W) and maps.is_contiguous()
+        B = maps.shape[0]
+        feats = out if out is not None else torch.empty(B, 512, device=self.device, dtype=torch.float32)
+        mb = max(1, min(self.micro_batch, B))
+        ws = self.workspace(mb)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_backbone_run', self._plan, _lib.ptr(maps), B, mb, _lib.ptr(feats), _lib.ptr(ws),
+                      ws.numel(), _lib.stream_handle(self.device))
+        return feats
+
+    def stem(self, maps: torch.Tensor) -> torch.Tensor:
+        B = maps.shape[0]
+        out = torch.empty(B, 128, 128, 64, device=self.device, dtype=self.tdtype)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_backbone_stem_run', self._plan, _lib.ptr(maps.contiguous()), B, _lib.ptr(out),
+                      _lib.stream_handle(self.device))
+        return out
+
+    def debug(self, maps: torch.Tensor):
+        """(pooled feats [B,512], layer4 map NHWC [B,16,16,512]) for small B."""
+        B = maps.shape[0]
+        feats = torch.empty(B, 512, device=self.device, dtype=torch.float32)
+        l4 = torch.empty(B, 16, 16, 512, device=self.device, dtype=self.tdtype)
+        ws = self.workspace(B)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_backbone_run_debug', self._plan, _lib.ptr(maps.contiguous()), B, _lib.ptr(feats),
+                      _lib.ptr(l4), _lib.ptr(ws), ws.numel(), _lib.stream_handle(self.device))
+        return feats, l4
+
+    def __del__(self):
+        try:
+            if getattr(self, '_plan', None):
+                _lib.load().sad_backbone_plan_destroy(self._plan)
+        except Exception:
+            pass
+
+
+class Heads:
+    """N BinaryClassifier heads (+ merge); ``head_sds[h]`` uses nn.Sequential
+    index keys (2.weight, 3.running_mean, ...)."""
+
+    def __init__(self, head_sds: Sequence[Dict[str, torch.Tensor]], feat_index: Sequence[int], n_feat: int,
+                 device='cuda'):
+        self.device = _dev(device)
+        self.n_heads = len(head_sds)
+        arrays = [_np32(sd[k]) for sd in head_sds for k in HEAD_KEYS]
+        self._keep = arrays
+        fi = (_lib.I32 * self.n_heads)(*feat_index)
+        self._plan = _lib.P()
+        with torch.cuda.device(self.device):
+            _lib.call('sad_heads_plan_create', _lib.pointer_array(arrays), self.n_heads, fi, n_feat,
+                      _lib.ctypes.byref(self._plan))
+        self.n_feat = n_feat
+        self._ws = None
+
+    def __call__(self, feats: Sequence[torch.Tensor], logits: torch.Tensor | None = None,
+                 merged: torch.Tensor | None = None):
+        B = feats[0].shape[0]
+        if logits is None:
+            logits = torch.empty(B, self.n_heads, 2, device=self.device, dtype=torch.float32)
+        if merged is None:
+            merged = torch.empty(B, self.n_heads + 1, device=self.device, dtype=torch.float32)
+        sz = _lib.SZ()
+        _lib.call('sad_heads_workspace_size', self._plan, B, _lib.ctypes.byref(sz))
+        if self._ws is None or self._ws.numel() < sz.value:
+            self._ws = torch.empty(sz.value, dtype=torch.uint8, device=self.device)
+        fp = (_lib.ctypes.c_void_p * self.n_feat)(*[f.data_ptr() for f in feats])
+        with torch.cuda.device(self.device):
+            _lib.call('sad_heads_merge_run', self._plan, fp, B, _lib.ptr(logits), _lib.ptr(merged),
+                      _lib.ptr(self._ws), self._ws.numel(), _lib.stream_handle(self.device))
+        return logits, merged
+
+    def __del__(self):
+        try:
+            if getattr(self, '_plan', None):
+                _lib.load().sad_heads_plan_destroy(self._plan)
+        except Exception:
+            pass
+
+
+def _digest(tensors: List[torch.Tensor]) -> str:
+    h = hashlib.sha1()
+    for t in tensors:
+        h.update(_np32(t).tobytes())
+    return h.hexdigest()
+
+
+def split_merged_state(sd: Dict[str, torch.Tensor]):
+    """merged state dict -> (sorted sub-model indices, {i: base_sd}, {i: head_sd}).
+    Index parsing follows inference_runner.py:88-98 (sorted ints after
+    ``sub_models.``)."""
+    idx = set()
+    for k in sd.keys():
+        parts = k.split('.')
+        if len(parts) >= 3 and parts[0] == 'sub_models':
+            try:
+                idx.add(int(parts[1]))
+            except ValueError:
+                pass
+    idx = sorted(idx)
+    bases, heads = {}, {}
+    for i in idx:
+        pre = f'sub_models.{i}.'
+        bases[i] = {k[len(pre) + 5:]: v for k, v in sd.items() if k.startswith(pre + 'base.')}
+        heads[i] = {k[len(pre) + 5:]: v for k, v in sd.items() if k.startswith(pre + 'head.')}
+    return idx, bases, heads
+
+
+class Engine:
+    """Merged checkpoint -> device pipeline  pcm -> (per-head logits, merged)."""
+
+    def __init__(self, merged_sd: Dict[str, torch.Tensor], device='cuda', dtype: str = 'bf16',
+                 micro_batch: int = 64, norm: str | None = 'slaney'):
+        self.device = _dev(device)
+        self.dtype = dtype
+        idx, bases, heads = split_merged_state(merged_sd)
+        if not idx:
+            raise ValueError('state dict has no sub_models.<i>.* keys')
+        self.indices = idx
+        digests, self.backbones, feat_index = {}, [], []
+        for i in idx:
+            keys = [k for k, _, kind in backbone_param_shapes()]
+            missing = [k for k in keys if not any(s.startswith(k + '.') for s in bases[i])]
+            if missing:
+                raise KeyError(f'sub-model {i} lacks backbone tensors {missing[:3]}...')
+            d = _digest([bases[i][k] for k in sorted(bases[i]) if not k.endswith('num_batches_tracked')])
+            if d not in digests:
+                digests[d] = len(self.backbones)
+                self.backbones.append(Backbone(bases[i], self.device, dtype, micro_batch))
+            feat_index.append(digests[d])
+        self.heads = Heads([heads[i] for i in idx], feat_index, len(self.backbones), self.device)
+        self.frontend = FrontEnd(self.device, norm=norm)
+        self.n_heads = len(idx)
+
+    def forward_maps(self, maps: torch.Tensor):
+        feats = [bb(maps) for bb in self.backbones]
+        return self.heads(feats)
+
+    def forward_pcm(self, pcm: torch.Tensor):
+        return self.forward_maps(self.frontend(pcm))

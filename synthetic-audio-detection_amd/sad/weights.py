@@ -100,8 +100,12 @@ def merged_state_dict(seed: int = 0, n_heads: int = 6, distinct_backbones: bool 
     quirk C2 situation) and head seed ``seed * 1000 + i + 1``.  ``bn_stats`` maps
     full keys (``sub_models.i....running_mean``) to arrays overriding defaults."""
     sd = OrderedDict()
+    cache = {}
     for i in range(n_heads):
-        bb = backbone_state_dict(seed + (i if distinct_backbones else 0))
+        bseed = seed + (i if distinct_backbones else 0)
+        if bseed not in cache:
+            cache[bseed] = backbone_state_dict(bseed)
+        bb = cache[bseed]
         for k, v in bb.items():
             sd[f'sub_models.{i}.base.{k}'] = v.clone()
         hd = head_state_dict(seed * 1000 + i + 1)
