@@ -48,6 +48,22 @@ struct DT<float> {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return (chunk ^ ((row >> 1) & 7)); }
 
+// One LDS-DMA wave-instruction: 16 B per lane from buffer offset `voff` to LDS
+// [lds_base + 16*lane].  M0 (compiler-reserved) is saved/restored inside the
+// statement; offsets past the buffer's num_records load zeros.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, int voff, unsigned lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(__builtin_amdgcn_readfirstlane(lds_base)), "s"(rsrc)
+      : "memory");
+}
+
 template <typename T>
 __device__ __forceinline__ void mfma_chunk(const uint4& a, const uint4& b, f32x4& acc);
 
@@ -64,86 +80,100 @@ __device__ __forceinline__ void mfma_chunk<float>(const uint4& a, const uint4& b
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
 }
 
+constexpr int CONV_STAGES = 3;
+
 template <int WM, int WN>
 constexpr int conv_smem_bytes() {
   constexpr int BM = 64 * WM, BN = 64 * WN;
-  constexpr int main_b = 2 * (BM + BN) * 128;
+  constexpr int main_b = CONV_STAGES * (BM + BN) * 128;
   constexpr int epi_b = BM * (BN + 4) * 4;
   return main_b > epi_b ? main_b : epi_b;
 }
 
 template <typename T, int WM, int WN>
-__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
+__global__ __launch_bounds__(64 * WM * WN, 1) void conv_igemm_kernel(ConvArgs a) {
+  constexpr int NW = WM * WN;               // waves per workgroup
+  constexpr int NT = 64 * NW;               // threads
   constexpr int BM = 64 * WM, BN = 64 * WN;
-  constexpr int EPC = DT<T>::EPC;
-  constexpr int BK = 8 * EPC;
-  constexpr int A_PER_T = BM / 32, B_PER_T = BN / 32;
+  constexpr int ES = sizeof(T);
+  constexpr int STAGE = (BM + BN) * 128;    // bytes per ring stage
+  constexpr int QA = BM / 8 / NW;           // A LDS-DMA wave-instructions per wave per K-step
+  constexpr int QB = BN / 8 / NW;           // B ...
+  static_assert(QA * 8 * NW == BM && QB * 8 * NW == BN, "tile/wave mismatch");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int n_tn = a.Cout / BN;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int tn = wg % n_tn, tm = wg / n_tn;
   const int64_t m0 = (int64_t)tm * BM;
   const int n0 = tn * BN;
-
-  const T* __restrict__ in = (const T*)a.in;
-  const T* __restrict__ wt = (const T*)a.wt;
-  const int ch = tid & 7, rbase = tid >> 3;
   const int HoWo = a.Ho * a.Wo;
 
-  // per-thread A rows: base pointer at tap (0,0), input origin, validity
-  const T* arow[A_PER_T];
-  int aiy[A_PER_T], aix[A_PER_T];
+  // Buffer resources: 32-bit byte offsets; an offset past num_records reads 0,
+  // which implements the conv zero padding without branches.
+  const __amdgpu_buffer_rsrc_t rin =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.in, (short)0, (int)a.in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rwt =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, (int)a.wt_bytes, 0x00020000);
+  const int pstride_b = (int)a.in_pstride * ES;
+
+  // LDS-DMA writes lane-linearly (dest = wave base + 16*lane), so the XOR
+  // swizzle is applied on the SOURCE: lane L of the wave-instruction that fills
+  // rows 8q..8q+7 loads chunk (L&7) ^ swzkey(row) of row 8q + (L>>3).
+  const int lrow = lane >> 3;
+  // A rows of this lane: q = wave + NW*i, row = 8q + lrow
+  int aoff[QA], aiy[QA], aix[QA];
 #pragma unroll
-  for (int i = 0; i < A_PER_T; ++i) {
-    const int64_t m = m0 + rbase + 32 * i;
+  for (int i = 0; i < QA; ++i) {
+    const int r = 8 * (wave + NW * i) + lrow;
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int64_t m = m0 + r;
     if (m < a.M) {
       const int b = (int)(m / HoWo);
       const int rem = (int)(m - (int64_t)b * HoWo);
-      const int oy = rem / a.Wo, ox = rem - (rem / a.Wo) * a.Wo;
+      const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
       aiy[i] = oy * a.stride - a.pad;
       aix[i] = ox * a.stride - a.pad;
-      arow[i] = in + (((int64_t)b * a.H + aiy[i]) * a.W + aix[i]) * a.in_pstride + ch * EPC;
+      aoff[i] = ((b * a.H + aiy[i]) * a.W + aix[i]) * pstride_b + c * 16;
     } else {
-      aiy[i] = -100000;
-      aix[i] = -100000;
-      arow[i] = in;
+      aiy[i] = -0x4000;
+      aix[i] = -0x4000;
+      aoff[i] = 0;
     }
   }
-  const int64_t Ktot = (int64_t)a.KH * a.KW * a.Cin;
-  const T* brow = wt + (int64_t)(n0 + rbase) * Ktot + ch * EPC;
-  const int cpt = a.Cin / BK;
+  const int ktot_b = a.KH * a.KW * a.Cin * ES;
+  int boff[QB];
+#pragma unroll
+  for (int i = 0; i < QB; ++i) {
+    const int r = 8 * (wave + NW * i) + lrow;           // row within the B tile
+    const int c = (lane & 7) ^ (((r + BM) >> 1) & 7);   // swizzle key of LDS row BM + r
+    boff[i] = (n0 + r) * ktot_b + c * 16;
+  }
+  const int cpt = a.Cin / (128 / ES);
   const int nk = a.KH * a.KW * cpt;
 
-  uint4 ra[A_PER_T], rb[B_PER_T];
-  auto gload = [&](int ks) {
+  // LDS byte address of the ring (M0 operand of the DMA)
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  // Issue the LDS-DMA for K-step ks into ring stage st.  Inline asm keeps the
+  // DMA out of hipcc's vmcnt bookkeeping (which would otherwise drain it with
+  // vmcnt(0) before the next ds_read); the loop counts vmcnt by hand.
+  auto issue = [&](int ks, int st) __attribute__((always_inline)) {
     const int tap = ks / cpt;
-    const int ci0 = (ks - tap * cpt) * BK;
-    const int ky = tap / a.KW, kx = tap - (tap / a.KW) * a.KW;
-    const int64_t toff = ((int64_t)ky * a.W + kx) * a.in_pstride + ci0;
+    const int ci0 = ks - tap * cpt;
+    const int ky = tap / a.KW, kx = tap - ky * a.KW;
+    const int toff = (ky * a.W + kx) * pstride_b + ci0 * 128;
+    const unsigned sb = lds0 + st * STAGE;
 #pragma unroll
-    for (int i = 0; i < A_PER_T; ++i) {
+    for (int i = 0; i < QA; ++i) {
       const int iy = aiy[i] + ky, ix = aix[i] + kx;
       const bool ok = ((unsigned)iy < (unsigned)a.H) && ((unsigned)ix < (unsigned)a.W);
-      ra[i] = ok ? *(const uint4*)(arow[i] + toff) : make_uint4(0, 0, 0, 0);
+      dma16(rin, ok ? aoff[i] + toff : 0x7FFFFFF0, sb + (wave + NW * i) * 1024);
     }
 #pragma unroll
-    for (int i = 0; i < B_PER_T; ++i) rb[i] = *(const uint4*)(brow + (int64_t)32 * i * Ktot + (int64_t)ks * BK);
-  };
-  auto sstore = [&](int buf) {
-    char* base = smem + buf * (BM + BN) * 128;
-#pragma unroll
-    for (int i = 0; i < A_PER_T; ++i) {
-      const int r = rbase + 32 * i;
-      *(uint4*)(base + r * 128 + (swz(r, ch) << 4)) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER_T; ++i) {
-      const int r = BM + rbase + 32 * i;
-      *(uint4*)(base + r * 128 + (swz(r, ch) << 4)) = rb[i];
-    }
+    for (int i = 0; i < QB; ++i) dma16(rwt, boff[i] + ks * 128, sb + BM * 128 + (wave + NW * i) * 1024);
   };
 
   f32x4 acc[4][4];
@@ -152,14 +182,21 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  gload(0);
-  sstore(0);
-  __syncthreads();
   const int fr = lane & 15, fg = lane >> 4;
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  int st = 0;
   for (int ks = 0; ks < nk; ++ks) {
-    const int cur = ks & 1;
-    if (ks + 1 < nk) gload(ks + 1);
-    const char* base = smem + cur * (BM + BN) * 128;
+    // retire this wave's DMA for step ks (step ks+1's stays in flight), then
+    // the barrier publishes every wave's step-ks DMA and frees stage (ks+2)%3
+    if (ks + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QA + QB) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + 2 < nk) issue(ks + 2, st == 0 ? 2 : st - 1);
+    const char* base = smem + st * STAGE;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       uint4 af[4], bfr[4];
@@ -179,9 +216,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) mfma_chunk<T>(af[i], bfr[j], acc[i][j]);
     }
-    if (ks + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
+    st = st == 2 ? 0 : st + 1;
   }
+  __syncthreads();
 
   // ---- epilogue: acc -> LDS [BM][BN+4] f32 -> bias/residual/relu -> store
   float* ep = (float*)smem;
@@ -195,7 +232,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         ep[(wm * 64 + i * 16 + fg * 4 + r) * LDE + wn * 64 + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
   constexpr int TPR = BN / 8;          // threads per output row (8 values each)
-  constexpr int RPP = 256 / TPR;       // rows per pass
+  constexpr int RPP = NT / TPR;        // rows per pass
   const int c8 = (tid % TPR) * 8;
   const float4 bias0 = *(const float4*)(a.bias + n0 + c8);
   const float4 bias1 = *(const float4*)(a.bias + n0 + c8 + 4);
@@ -426,21 +463,27 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
 }
 
 // --------------------------------------------------------------- avgpool --
-// [B, HW, C] (NHWC, dtype T) -> [B, C] fp32 mean over HW.
+// [B, HW, C] (NHWC, dtype T) -> [B, C] fp32 mean over HW.  Workgroup = one
+// segment x 64 channels; 4 waves split the pixels, LDS combine.
 template <typename T>
 __global__ __launch_bounds__(256) void avgpool_kernel(const T* __restrict__ in, int hw, int c,
                                                       float* __restrict__ out) {
+  __shared__ float part[4][64];
   const int64_t b = blockIdx.x;
-  for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
-    float s = 0.f;
-    const T* p = in + b * hw * c + ch;
-    for (int i = 0; i < hw; ++i) {
-      if constexpr (sizeof(T) == 2)
-        s += bf2f(p[(int64_t)i * c]);
-      else
-        s += p[(int64_t)i * c];
-    }
-    out[b * c + ch] = s / (float)hw;
+  const int ch = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  const T* p = in + b * hw * c + ch;
+  float s = 0.f;
+  for (int i = g; i < hw; i += 4) {
+    if constexpr (sizeof(T) == 2)
+      s += bf2f(p[(int64_t)i * c]);
+    else
+      s += p[(int64_t)i * c];
+  }
+  part[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0) {
+    const int t = threadIdx.x;
+    out[b * c + ch] = ((part[0][t] + part[1][t]) + (part[2][t] + part[3][t])) / (float)hw;
   }
 }
 
@@ -458,21 +501,26 @@ static int launch_conv_t(const ConvArgs& a, hipStream_t s) {
   const int64_t tiles_m = (a.M + BM - 1) / BM;
   const int64_t nwg = tiles_m * (a.Cout / BN);
   SAD_REQUIRE(nwg < (1ll << 31), "grid too large");
-  hipLaunchKernelGGL((conv_igemm_kernel<T, WM, WN>), dim3((unsigned)nwg), dim3(256), smem, s, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<T, WM, WN>), dim3((unsigned)nwg), dim3(64 * WM * WN), smem, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }
 
-int launch_conv(const ConvArgs& a, int dtype, hipStream_t s) {
+int launch_conv(const ConvArgs& a_in, int dtype, hipStream_t s) {
   const int EPC = dtype == SAD_BF16 ? 8 : 4;
+  const int ES = dtype == SAD_BF16 ? 2 : 4;
+  ConvArgs a = a_in;
+  a.in_bytes = (((int64_t)a.N * a.H * a.W - 1) * a.in_pstride + a.Cin) * ES;
+  a.wt_bytes = (int64_t)a.Cout * a.KH * a.KW * a.Cin * ES;
+  SAD_REQUIRE(a.in_bytes < (1ll << 31) - 64 && a.wt_bytes < (1ll << 31), "conv operand exceeds the 2 GiB buffer range (lower the micro-batch)");
   SAD_REQUIRE(a.Cin % (8 * EPC) == 0, "Cin must be a multiple of the K-step");
   SAD_REQUIRE(a.Cout % 64 == 0, "Cout must be a multiple of 64");
   SAD_REQUIRE(a.in_pstride % EPC == 0 && a.out_pstride % 8 == 0, "pixel strides must keep 16-B alignment");
-  // tile choice: 128x128 when Cout allows, else 256x64
+  // tile choice: 256x128 (8 waves) when Cout allows, else 256x64 (4 waves)
   const bool wide = a.Cout % 128 == 0;
   if (dtype == SAD_BF16)
-    return wide ? launch_conv_t<u16, 2, 2>(a, s) : launch_conv_t<u16, 4, 1>(a, s);
-  return wide ? launch_conv_t<float, 2, 2>(a, s) : launch_conv_t<float, 4, 1>(a, s);
+    return wide ? launch_conv_t<u16, 4, 2>(a, s) : launch_conv_t<u16, 4, 1>(a, s);
+  return wide ? launch_conv_t<float, 4, 2>(a, s) : launch_conv_t<float, 4, 1>(a, s);
 }
 
 int launch_stem(const StemArgs& a, int dtype, hipStream_t s) {
@@ -489,9 +537,9 @@ int launch_stem(const StemArgs& a, int dtype, hipStream_t s) {
 int launch_avgpool(const void* in, int64_t B, int hw, int c, float* out, int dtype, hipStream_t s) {
   if (B == 0) return SAD_OK;
   if (dtype == SAD_BF16)
-    hipLaunchKernelGGL(avgpool_kernel<u16>, dim3((unsigned)B), dim3(256), 0, s, (const u16*)in, hw, c, out);
+    hipLaunchKernelGGL(avgpool_kernel<u16>, dim3((unsigned)B, c / 64), dim3(256), 0, s, (const u16*)in, hw, c, out);
   else
-    hipLaunchKernelGGL(avgpool_kernel<float>, dim3((unsigned)B), dim3(256), 0, s, (const float*)in, hw, c, out);
+    hipLaunchKernelGGL(avgpool_kernel<float>, dim3((unsigned)B, c / 64), dim3(256), 0, s, (const float*)in, hw, c, out);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }

@@ -17,6 +17,8 @@ struct ConvArgs {
   int Ho, Wo, Cout, KH, KW, stride, pad;
   int relu;
   int64_t M;             // N * Ho * Wo
+  int64_t in_bytes;      // set by launch_conv: addressable input span (buffer range)
+  int64_t wt_bytes;      // set by launch_conv
 };
 
 struct StemArgs {
