@@ -67,7 +67,7 @@ def main():
     ap.add_argument('--batch', type=int, default=2048, help='segments per GPU per step')
     ap.add_argument('--heads', type=int, default=6)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
-    ap.add_argument('--micro-batch', type=int, default=64)
+    ap.add_argument('--micro-batch', type=int, default=128)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
 

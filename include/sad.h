@@ -144,6 +144,19 @@ int sad_heads_merge_run(const sad_heads_plan* plan, const float* const* feats, i
                         float* logits, float* merged, void* workspace, size_t ws_bytes,
                         void* stream);
 
+/* ------------------------------------------------------------- operators */
+/* One NHWC convolution (+ folded-BN bias, optional residual add, optional
+ * ReLU) on the implicit-GEMM MFMA kernel the backbone uses: the building block
+ * of timm's BasicBlock (conv -> bn -> [+ shortcut] -> act).  Exposed for op-level
+ * parity tests and tile tuning.
+ * in [N,H,W,Cin], wt [Cout,k,k,Cin] (dtype), bias [Cout] fp32, res/out
+ * [N,Ho,Wo,Cout] (dtype; res may be NULL), Ho = (H + 2 pad - k)/stride + 1.
+ * variant: 0 = the backbone's choice, 1..8 = tile variants (csrc/conv.hip). */
+int sad_conv2d_run(const void* in, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* wt,
+                   const float* bias, const void* res, void* out, int32_t Cout, int32_t k,
+                   int32_t stride, int32_t pad, int32_t relu, int32_t dtype, int32_t variant,
+                   void* stream);
+
 /* -------------------------------------------------------------- synthetic */
 /* Deterministic synthetic segments; bit-identical to
  * sad/synth.py up to rare 1-LSB float64 libm differences in the tone term.

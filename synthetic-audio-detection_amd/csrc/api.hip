@@ -133,7 +133,8 @@ extern "C" int sad_backbone_plan_create(const float* const* params, int32_t n_pa
       for (int k = 0; k < 49; ++k) {
         double s = 0.0;
         for (int c = 0; c < 3; ++c) s += (double)W[(co * 3 + c) * 49 + k];
-        const int pos = dtype == SAD_BF16 ? k : ((k & 3) * 16 + (k >> 2));  // f32: k=4q+g at g*16+q
+        // bf16 stem: (ky, kx) on an 8x8 grid; f32 stem: k = ky*7+kx, k=4q+g at g*16+q
+        const int pos = dtype == SAD_BF16 ? (k / 7) * 8 + (k % 7) : ((k & 3) * 16 + (k >> 2));
         w[co * 64 + pos] = s * sc[co];
       }
       b[co] = sh[co];
@@ -450,4 +451,36 @@ extern "C" int sad_heads_merge_run(const sad_heads_plan* p, const float* const* 
     if ((rc = launch_conv(a, SAD_F32, s))) return rc;
   }
   return launch_heads_final(y2, B, N, p->w3, p->b3, logits, merged, s);
+}
+
+// ------------------------------------------------------------- operators ----
+extern "C" int sad_conv2d_run(const void* in, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* wt,
+                              const float* bias, const void* res, void* out, int32_t Cout, int32_t k,
+                              int32_t stride, int32_t pad, int32_t relu, int32_t dtype, int32_t variant,
+                              void* stream) {
+  SAD_REQUIRE(in && wt && bias && out, "null tensor");
+  SAD_REQUIRE(N >= 0 && H > 0 && W > 0 && k > 0 && stride > 0 && pad >= 0, "bad shape");
+  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
+  ConvArgs a{};
+  a.in = in;
+  a.in_pstride = Cin;
+  a.N = (int)N;
+  a.H = H;
+  a.W = W;
+  a.Cin = Cin;
+  a.wt = wt;
+  a.bias = bias;
+  a.res = res;
+  a.res_pstride = Cout;
+  a.out = out;
+  a.out_pstride = Cout;
+  a.Ho = (H + 2 * pad - k) / stride + 1;
+  a.Wo = (W + 2 * pad - k) / stride + 1;
+  a.Cout = Cout;
+  a.KH = a.KW = k;
+  a.stride = stride;
+  a.pad = pad;
+  a.relu = relu;
+  a.M = N * a.Ho * a.Wo;
+  return launch_conv(a, dtype, (hipStream_t)stream, variant);
 }

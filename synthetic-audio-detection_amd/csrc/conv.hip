@@ -80,18 +80,19 @@ __device__ __forceinline__ void mfma_chunk<float>(const uint4& a, const uint4& b
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
 }
 
-constexpr int CONV_STAGES = 3;
-
-template <int WM, int WN>
+template <int WM, int WN, int S>
 constexpr int conv_smem_bytes() {
   constexpr int BM = 64 * WM, BN = 64 * WN;
-  constexpr int main_b = CONV_STAGES * (BM + BN) * 128;
+  constexpr int main_b = S * (BM + BN) * 128;
   constexpr int epi_b = BM * (BN + 4) * 4;
   return main_b > epi_b ? main_b : epi_b;
 }
 
-template <typename T, int WM, int WN>
+// S = LDS ring stages (prefetch depth S-1): 3 at one workgroup per CU, 2 when
+// two workgroups share a CU.
+template <typename T, int WM, int WN, int S>
 __global__ __launch_bounds__(64 * WM * WN, 1) void conv_igemm_kernel(ConvArgs a) {
+  static_assert(S == 2 || S == 3, "ring depth");
   constexpr int NW = WM * WN;               // waves per workgroup
   constexpr int NT = 64 * NW;               // threads
   constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -184,18 +185,19 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_igemm_kernel(ConvArgs a)
 
   const int fr = lane & 15, fg = lane >> 4;
   issue(0, 0);
-  if (nk > 1) issue(1, 1);
+  if (S == 3 && nk > 1) issue(1, 1);
   int st = 0;
   for (int ks = 0; ks < nk; ++ks) {
-    // retire this wave's DMA for step ks (step ks+1's stays in flight), then
-    // the barrier publishes every wave's step-ks DMA and frees stage (ks+2)%3
-    if (ks + 1 < nk)
+    // retire this wave's DMA for step ks (with S = 3, step ks+1's stays in
+    // flight), then the barrier publishes every wave's step-ks DMA and frees
+    // the stage the next issue overwrites (read by step ks-1)
+    if (S == 3 && ks + 1 < nk)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QA + QB) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (ks + 2 < nk) issue(ks + 2, st == 0 ? 2 : st - 1);
+    if (ks + S - 1 < nk) issue(ks + S - 1, S == 3 ? (st == 0 ? 2 : st - 1) : (st ^ 1));
     const char* base = smem + st * STAGE;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_igemm_kernel(ConvArgs a)
 #pragma unroll
         for (int j = 0; j < 4; ++j) mfma_chunk<T>(af[i], bfr[j], acc[i][j]);
     }
-    st = st == 2 ? 0 : st + 1;
+    st = st + 1 == S ? 0 : st + 1;
   }
   __syncthreads();
 
@@ -462,6 +464,136 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
   }
 }
 
+// ------------------------------------------------------------ stem, bf16 --
+// Throughput-mode stem.  K is laid out (ky, kx) on an 8 x 8 grid (ky = 7 and
+// kx = 7 carry zero weights), so the 8 consecutive k of one MFMA lane fragment
+// are 8 consecutive image pixels of ONE row: 4 x ds_read_b32 from a bf16 image
+// band (row pitch 272 dwords = 16 banks mod 32, conflict-free for the 4 lane
+// groups).  A workgroup produces STEM_P pooled rows: conv rows 2*py0-1 ..
+// 2*(py0+P)-1 (2P+1 rows for P pooled rows), vertical max carried in registers.
+constexpr int STEM_P = 4;
+constexpr int STEM_BAND_ROWS = 4 * STEM_P + 8;
+constexpr int STEM_BPITCH = 544;  // bf16 elements per band row (>= 518)
+
+__global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 s_img[STEM_BAND_ROWS * STEM_BPITCH];
+  __shared__ __attribute__((aligned(16))) u16 s_w[64 * 72];
+  __shared__ __attribute__((aligned(16))) u16 s_pool[256 * 64];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int py0 = blockIdx.x * STEM_P;
+  const int64_t b = blockIdx.y;
+  const float* __restrict__ map = a.map + b * a.mh * a.mw;
+  for (int i = tid; i < 64 * 8; i += 256) {  // [64 co][64 k] bf16 -> pitch 72
+    const int co = i >> 3, c8 = (i & 7) * 8;
+    *(uint4*)(s_w + co * 72 + c8) = *(const uint4*)((const u16*)a.w + co * 64 + c8);
+  }
+  // image band: rows iy = 4*py0 - 5 + tr, cols ix = tc - 3 (zero outside 512x512)
+  const float sh = (float)a.mh / 512.f, sw = (float)a.mw / 512.f;
+  for (int i = tid; i < STEM_BAND_ROWS * STEM_BPITCH; i += 256) {
+    const int tr = i / STEM_BPITCH, tc = i - tr * STEM_BPITCH;
+    const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
+    float v = 0.f;
+    if ((unsigned)iy < 512u && (unsigned)ix < 512u) {
+      float fy = sh * (iy + 0.5f) - 0.5f;
+      fy = fy < 0.f ? 0.f : fy;
+      float fx = sw * (ix + 0.5f) - 0.5f;
+      fx = fx < 0.f ? 0.f : fx;
+      const int y0 = min((int)floorf(fy), a.mh - 1), x0 = min((int)floorf(fx), a.mw - 1);
+      const int y1 = min(y0 + 1, a.mh - 1), x1 = min(x0 + 1, a.mw - 1);
+      const float ly = fminf(fmaxf(fy - y0, 0.f), 1.f), lx = fminf(fmaxf(fx - x0, 0.f), 1.f);
+      v = (1.f - ly) * ((1.f - lx) * map[y0 * a.mw + x0] + lx * map[y0 * a.mw + x1]) +
+          ly * ((1.f - lx) * map[y1 * a.mw + x0] + lx * map[y1 * a.mw + x1]);
+    }
+    s_img[i] = f2bf(v);
+  }
+  __syncthreads();
+  const int fr = lane & 15, fg = lane >> 4;
+  uint4 bw[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) bw[j][s] = *(const uint4*)(s_w + (j * 16 + fr) * 72 + 32 * s + 8 * fg);
+  float bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bias[j] = a.bias[j * 16 + fr];
+
+  // conv row cr (relative band row of its first tap = 2*(cr - 2*py0) + 2)
+  auto conv_row = [&](int cr, f32x4 (&r)[4][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (cr < 0 || cr >= 256) return;  // block-uniform; zero row never wins the max
+    const int rb = 2 * (cr - 2 * py0) + 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cx = wave * 64 + i * 16 + fr;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const u16* p = s_img + (rb + 4 * s + fg) * STEM_BPITCH + 2 * cx;
+        uint4 av;
+        av.x = *(const uint32_t*)(p + 0);
+        av.y = *(const uint32_t*)(p + 2);
+        av.z = *(const uint32_t*)(p + 4);
+        av.w = *(const uint32_t*)(p + 6);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mfma_chunk<u16>(av, bw[j][s], r[i][j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[i][j][e] = bf2f(f2bf(fmaxf(r[i][j][e] + bias[j], 0.f)));
+  };
+
+  f32x4 carry[4][4], cur[4][4];
+  conv_row(2 * py0 - 1, carry);
+  for (int pi = 0; pi < STEM_P; ++pi) {
+    const int py = py0 + pi;
+    conv_row(2 * py, cur);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cur[i][j][e] = fmaxf(carry[i][j][e], cur[i][j][e]);
+    conv_row(2 * py + 1, carry);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          s_pool[(wave * 64 + i * 16 + fg * 4 + e) * 64 + j * 16 + fr] = f2bf(fmaxf(cur[i][j][e], carry[i][j][e]));
+    __syncthreads();
+    u16* __restrict__ out = (u16*)a.out + ((b * 128 + py) * 128) * 64;
+    for (int it = tid; it < 128 * 8; it += 256) {
+      const int q = it >> 3, c0 = (it & 7) * 8;
+      float m[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[e] = 0.f;
+#pragma unroll
+      for (int d = -1; d <= 1; ++d) {
+        const int px = 2 * q + d;
+        if (px < 0) continue;  // px <= 255 always
+        const uint4 v = *(const uint4*)(s_pool + px * 64 + c0);
+        const u16* h = (const u16*)&v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], bf2f(h[e]));
+      }
+      uint4 qv;
+      u16* h = (u16*)&qv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) h[e] = f2bf(m[e]);
+      *(uint4*)(out + q * 64 + c0) = qv;
+    }
+    __syncthreads();
+  }
+}
+
 // --------------------------------------------------------------- avgpool --
 // [B, HW, C] (NHWC, dtype T) -> [B, C] fp32 mean over HW.  Workgroup = one
 // segment x 64 channels; 4 waves split the pixels, LDS combine.
@@ -488,46 +620,69 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const T* __restrict__ in, 
 }
 
 // ---------------------------------------------------------------- launch --
-template <typename T, int WM, int WN>
+template <typename T, int WM, int WN, int S>
 static int launch_conv_t(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
-  constexpr int smem = conv_smem_bytes<WM, WN>();
+  constexpr int smem = conv_smem_bytes<WM, WN, S>();
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<T, WM, WN>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<T, WM, WN, S>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
+  SAD_REQUIRE(a.Cout % BN == 0, "Cout must be a multiple of the tile width");
   const int64_t tiles_m = (a.M + BM - 1) / BM;
   const int64_t nwg = tiles_m * (a.Cout / BN);
   SAD_REQUIRE(nwg < (1ll << 31), "grid too large");
-  hipLaunchKernelGGL((conv_igemm_kernel<T, WM, WN>), dim3((unsigned)nwg), dim3(64 * WM * WN), smem, s, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<T, WM, WN, S>), dim3((unsigned)nwg), dim3(64 * WM * WN), smem, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }
 
-int launch_conv(const ConvArgs& a_in, int dtype, hipStream_t s) {
+// Tile variants (BM x BN, waves, ring stages, LDS):
+//  1: 256x64  4w S3 120 KB      2: 256x64  4w S2  80 KB (2 WG/CU)
+//  3: 256x128 8w S3 144 KB      4: 128x128 4w S3  96 KB
+//  5: 128x128 4w S2  64 KB      6: 512x64  8w S2 144 KB
+//  7: 128x64  2w S3  72 KB      8: 256x128 8w S2  96 KB
+template <typename T>
+static int launch_conv_v(const ConvArgs& a, int v, hipStream_t s) {
+  switch (v) {
+    case 1: return launch_conv_t<T, 4, 1, 3>(a, s);
+    case 2: return launch_conv_t<T, 4, 1, 2>(a, s);
+    case 3: return launch_conv_t<T, 4, 2, 3>(a, s);
+    case 4: return launch_conv_t<T, 2, 2, 3>(a, s);
+    case 5: return launch_conv_t<T, 2, 2, 2>(a, s);
+    case 6: return launch_conv_t<T, 8, 1, 2>(a, s);
+    case 7: return launch_conv_t<T, 2, 1, 3>(a, s);
+    case 8: return launch_conv_t<T, 4, 2, 2>(a, s);
+  }
+  set_error("unknown conv variant");
+  return SAD_ERR_ARG;
+}
+
+int default_conv_variant(const ConvArgs& a) { return a.Cout % 128 == 0 ? 5 : 2; }
+
+int launch_conv(const ConvArgs& a_in, int dtype, hipStream_t s, int variant) {
   const int EPC = dtype == SAD_BF16 ? 8 : 4;
   const int ES = dtype == SAD_BF16 ? 2 : 4;
   ConvArgs a = a_in;
   a.in_bytes = (((int64_t)a.N * a.H * a.W - 1) * a.in_pstride + a.Cin) * ES;
   a.wt_bytes = (int64_t)a.Cout * a.KH * a.KW * a.Cin * ES;
-  SAD_REQUIRE(a.in_bytes < (1ll << 31) - 64 && a.wt_bytes < (1ll << 31), "conv operand exceeds the 2 GiB buffer range (lower the micro-batch)");
+  SAD_REQUIRE(a.in_bytes < (1ll << 31) - 64 && a.wt_bytes < (1ll << 31),
+              "conv operand exceeds the 2 GiB buffer range (lower the micro-batch)");
   SAD_REQUIRE(a.Cin % (8 * EPC) == 0, "Cin must be a multiple of the K-step");
   SAD_REQUIRE(a.Cout % 64 == 0, "Cout must be a multiple of 64");
   SAD_REQUIRE(a.in_pstride % EPC == 0 && a.out_pstride % 8 == 0, "pixel strides must keep 16-B alignment");
-  // tile choice: 256x128 (8 waves) when Cout allows, else 256x64 (4 waves)
-  const bool wide = a.Cout % 128 == 0;
-  if (dtype == SAD_BF16)
-    return wide ? launch_conv_t<u16, 4, 2>(a, s) : launch_conv_t<u16, 4, 1>(a, s);
-  return wide ? launch_conv_t<float, 4, 2>(a, s) : launch_conv_t<float, 4, 1>(a, s);
+  if (a.M == 0) return SAD_OK;
+  const int v = variant > 0 ? variant : default_conv_variant(a);
+  return dtype == SAD_BF16 ? launch_conv_v<u16>(a, v, s) : launch_conv_v<float>(a, v, s);
 }
 
 int launch_stem(const StemArgs& a, int dtype, hipStream_t s) {
   SAD_REQUIRE(a.B <= 65535, "stem: B > 65535");
   if (a.B == 0) return SAD_OK;
   if (dtype == SAD_BF16)
-    hipLaunchKernelGGL(stem_kernel<u16>, dim3(128, (unsigned)a.B), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(stem_bf16_kernel, dim3(128 / STEM_P, (unsigned)a.B), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(stem_kernel<float>, dim3(128, (unsigned)a.B), dim3(256), 0, s, a);
   SAD_CHECK_HIP(hipGetLastError());

@@ -24,14 +24,16 @@ struct ConvArgs {
 struct StemArgs {
   const float* map;      // [B, mh, mw] standardised maps
   int mh, mw;
-  const void* w;         // [64 co][64 k] folded conv1 (k = ky*7+kx, zero for k >= 49),
+  const void* w;         // [64 co][64 k] folded conv1; bf16: k = ky*8+kx (7x7 in an 8x8 grid),
+                         // f32: k = ky*7+kx (zero for k >= 49),
                          // f32 variant permuted: position g*16+q holds k = 4q+g
   const float* bias;     // [64]
   void* out;             // NHWC [B, 128, 128, 64]
   int64_t B;
 };
 
-int launch_conv(const ConvArgs& a, int dtype, hipStream_t s);
+int launch_conv(const ConvArgs& a, int dtype, hipStream_t s, int variant = 0);
+int default_conv_variant(const ConvArgs& a);
 int launch_stem(const StemArgs& a, int dtype, hipStream_t s);
 int launch_avgpool(const void* in, int64_t B, int hw, int c, float* out, int dtype, hipStream_t s);
 int launch_heads_final(const float* y2, int64_t B, int n_heads, const float* w3, const float* b3,

@@ -54,6 +54,7 @@ SIGNATURES = {
     'sad_heads_plan_destroy': (ctypes.c_int, [P]),
     'sad_heads_workspace_size': (ctypes.c_int, [P, I64, ctypes.POINTER(SZ)]),
     'sad_heads_merge_run': (ctypes.c_int, [P, FPP, I64, P, P, P, SZ, P]),
+    'sad_conv2d_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P]),
     'sad_synth_pcm': (ctypes.c_int, [ctypes.c_uint64, I64, I64, I32, P, P]),
 }
 

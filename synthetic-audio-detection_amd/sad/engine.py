@@ -264,3 +264,20 @@ class Engine:
 
     def forward_pcm(self, pcm: torch.Tensor):
         return self.forward_maps(self.frontend(pcm))
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int = 1, pad: int = 0,
+           res: torch.Tensor | None = None, relu: bool = True, variant: int = 0,
+           out: torch.Tensor | None = None) -> torch.Tensor:
+    """NHWC conv on the libsad implicit-GEMM kernel.  x [N,H,W,Cin] bf16|fp32,
+    w [Cout,k,k,Cin] same dtype, bias [Cout] fp32, res [N,Ho,Wo,Cout] or None."""
+    N, H, W, Cin = x.shape
+    Cout, k = w.shape[0], w.shape[1]
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    dt = _lib.SAD_BF16 if x.dtype == torch.bfloat16 else _lib.SAD_F32
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Cout, device=x.device, dtype=x.dtype)
+    with torch.cuda.device(x.device):
+        _lib.call('sad_conv2d_run', _lib.ptr(x), N, H, W, Cin, _lib.ptr(w), _lib.ptr(bias), _lib.ptr(res),
+                  _lib.ptr(out), Cout, k, stride, pad, int(relu), dt, variant, _lib.stream_handle(x.device))
+    return out

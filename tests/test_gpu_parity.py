@@ -97,6 +97,23 @@ def test_stem_fp32_vs_oracle(golden_frontend):
     assert err <= 1e-5
 
 
+def test_stem_bf16_vs_oracle(golden_frontend):
+    """bf16 stem (8x8 tap grid, LDS band, register vertical max) vs the fp32 oracle."""
+    from oracle import frontend as ofe
+    from sad.engine import Backbone, split_merged_state
+    _, bases, _ = split_merged_state(merged_sd('n6'))
+    bb = Backbone(bases[0], DEV, 'bf16')
+    maps = torch.from_numpy(golden_frontend['std_map'])
+    out = bb.stem(maps.to(DEV)).float().cpu()
+    base = _oracle_sub('n6').base
+    with torch.no_grad():
+        img = ofe.resize_bilinear(maps.unsqueeze(1), (512, 512)).repeat(1, 3, 1, 1)
+        ref = base.maxpool(base.act1(base.bn1(base.conv1(img)))).permute(0, 2, 3, 1)
+    err = ((out - ref).abs().max() / ref.abs().max()).item()
+    print(f'stem bf16 rel err {err:.3e}')
+    assert err <= 2e-2
+
+
 @pytest.mark.parametrize('dtype,tol', [('fp32', 1e-4), ('bf16', 6e-2)])
 def test_backbone_vs_oracle(golden_frontend, golden_models, dtype, tol):
     from sad.engine import Backbone, split_merged_state
