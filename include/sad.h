@@ -83,6 +83,10 @@ int sad_frontend_frames(const sad_frontend_plan* plan, int32_t* n_frames);
  *          (x - mean) / (std_unbiased + 1e-6), per segment. */
 int sad_frontend_run(const sad_frontend_plan* plan, const int16_t* pcm, int64_t n_seg,
                      int64_t seg_stride, float* out_db, float* out_map, void* stream);
+/* Same on fp32 waveforms already in [-1, 1) (the reference's tensor after
+ * mono averaging / resampling, preprocess_waveform at inference_runner.py:144-155). */
+int sad_frontend_run_f32(const sad_frontend_plan* plan, const float* wav, int64_t n_seg,
+                         int64_t seg_stride, float* out_db, float* out_map, void* stream);
 
 /* Replaces torchvision.transforms.Resize((512,512)) + repeat(3,1,1)
  * (inference_runner.py:172-174) for callers that want the image itself:
@@ -114,6 +118,12 @@ int sad_backbone_workspace_size(const sad_backbone_plan* plan, int64_t micro_bat
 int sad_backbone_run(const sad_backbone_plan* plan, const float* map, int64_t B,
                      int64_t micro_batch, float* feats, void* workspace, size_t ws_bytes,
                      void* stream);
+/* Same from already-resized images: img [B, 512, 512] fp32 = ONE channel of
+ * the reference's [B, 3, 512, 512] input (its 3 channels are identical,
+ * inference_runner.py:173; the caller checks that). */
+int sad_backbone_run_img(const sad_backbone_plan* plan, const float* img, int64_t B,
+                         int64_t micro_batch, float* feats, void* workspace, size_t ws_bytes,
+                         void* stream);
 /* Debug/parity entry: run only the fused resize+stem (conv1+bn1+relu+maxpool)
  * on B maps, writing NHWC [B,128,128,64] in the plan's dtype. */
 int sad_backbone_stem_run(const sad_backbone_plan* plan, const float* map, int64_t B,

@@ -189,14 +189,14 @@ extern "C" int sad_backbone_workspace_size(const sad_backbone_plan* p, int64_t m
   return SAD_OK;
 }
 
-static int run_chunk(const sad_backbone_plan* p, const float* map, int64_t mb, float* feats,
+static int run_chunk(const sad_backbone_plan* p, const float* map, const float* img, int64_t mb, float* feats,
                      void* layer4_out, char* ws, hipStream_t s) {
   const size_t ab = act_bytes(p, mb);
   void* bufA = ws;
   void* bufB = ws + ab;
   void* bufT = ws + 2 * ab;
   void* bufD = ws + 3 * ab;
-  StemArgs st{map, p->mh, p->mw, p->stem_w, p->stem_b, bufA, mb};
+  StemArgs st{map, img, p->mh, p->mw, p->stem_w, p->stem_b, bufA, mb};
   int rc = launch_stem(st, p->dtype, s);
   if (rc) return rc;
   int H = 128, C = 64;
@@ -288,7 +288,7 @@ extern "C" int sad_backbone_run(const sad_backbone_plan* p, const float* map, in
   const int64_t plane = (int64_t)p->mh * p->mw;
   for (int64_t i = 0; i < B; i += mb) {
     const int64_t n = std::min(mb, B - i);
-    int rc = run_chunk(p, map + i * plane, n, feats + i * 512, nullptr, (char*)ws, (hipStream_t)stream);
+    int rc = run_chunk(p, map + i * plane, nullptr, n, feats + i * 512, nullptr, (char*)ws, (hipStream_t)stream);
     if (rc) return rc;
   }
   return SAD_OK;
@@ -303,14 +303,32 @@ extern "C" int sad_backbone_run_debug(const sad_backbone_plan* p, const float* m
     set_error("workspace too small (debug run needs micro_batch = B)");
     return SAD_ERR_NOMEM;
   }
-  return run_chunk(p, map, B, feats, layer4_out, (char*)ws, (hipStream_t)stream);
+  return run_chunk(p, map, nullptr, B, feats, layer4_out, (char*)ws, (hipStream_t)stream);
 }
 
 extern "C" int sad_backbone_stem_run(const sad_backbone_plan* p, const float* map, int64_t B, void* out,
                                      void* stream) {
   SAD_REQUIRE(p && map && out && B >= 0, "null args");
-  StemArgs st{map, p->mh, p->mw, p->stem_w, p->stem_b, out, B};
+  StemArgs st{map, nullptr, p->mh, p->mw, p->stem_w, p->stem_b, out, B};
   return launch_stem(st, p->dtype, (hipStream_t)stream);
+}
+
+extern "C" int sad_backbone_run_img(const sad_backbone_plan* p, const float* img, int64_t B, int64_t mb,
+                                    float* feats, void* ws, size_t ws_bytes, void* stream) {
+  SAD_REQUIRE(p && img && feats && ws, "null args");
+  SAD_REQUIRE(B >= 0 && mb > 0, "bad batch");
+  size_t need = 0;
+  sad_backbone_workspace_size(p, mb, &need);
+  if (ws_bytes < need) {
+    set_error("workspace too small");
+    return SAD_ERR_NOMEM;
+  }
+  for (int64_t i = 0; i < B; i += mb) {
+    const int64_t n = std::min(mb, B - i);
+    int rc = run_chunk(p, nullptr, img + i * 512 * 512, n, feats + i * 512, nullptr, (char*)ws, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return SAD_OK;
 }
 
 // ---------------------------------------------------------------- heads ----

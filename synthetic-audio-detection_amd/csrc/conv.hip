@@ -279,6 +279,21 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_igemm_kernel(ConvArgs a)
 }
 
 // ------------------------------------------------------------------- stem --
+// torchvision Resize((512,512)) sample (bilinear, align_corners=False; the
+// antialias filter is a no-op for this upsample) of an mh x mw map at (iy, ix).
+__device__ __forceinline__ float bilinear512(const float* __restrict__ map, int mh, int mw, float sh, float sw,
+                                            int iy, int ix) {
+  float fy = sh * (iy + 0.5f) - 0.5f;
+  fy = fy < 0.f ? 0.f : fy;
+  float fx = sw * (ix + 0.5f) - 0.5f;
+  fx = fx < 0.f ? 0.f : fx;
+  const int y0 = min((int)floorf(fy), mh - 1), x0 = min((int)floorf(fx), mw - 1);
+  const int y1 = min(y0 + 1, mh - 1), x1 = min(x0 + 1, mw - 1);
+  const float ly = fminf(fmaxf(fy - y0, 0.f), 1.f), lx = fminf(fmaxf(fx - x0, 0.f), 1.f);
+  return (1.f - ly) * ((1.f - lx) * map[y0 * mw + x0] + lx * map[y0 * mw + x1]) +
+         ly * ((1.f - lx) * map[y1 * mw + x0] + lx * map[y1 * mw + x1]);
+}
+
 constexpr int STEM_IMG_ROWS = 11;
 constexpr int STEM_IMG_PITCH = 520;  // >= 517 columns (ix + 3 in [0, 517))
 
@@ -293,7 +308,7 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int py = blockIdx.x;          // pooled row 0..127
   const int64_t b = blockIdx.y;       // image
-  const float* __restrict__ map = a.map + b * a.mh * a.mw;
+  const float* __restrict__ map = a.img ? nullptr : a.map + b * a.mh * a.mw;
 
   // weights -> LDS (already in the per-dtype k order, see plan)
   for (int i = tid; i < 64 * 64; i += 256) s_w[(i >> 6) * WPITCH + (i & 63)] = ((const T*)a.w)[i];
@@ -304,15 +319,7 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
     const int iy = 4 * py - 5 + tr, ix = tc - 3;
     float v = 0.f;
     if ((unsigned)iy < 512u && (unsigned)ix < 512u) {
-      float fy = sh * (iy + 0.5f) - 0.5f;
-      fy = fy < 0.f ? 0.f : fy;
-      float fx = sw * (ix + 0.5f) - 0.5f;
-      fx = fx < 0.f ? 0.f : fx;
-      const int y0 = min((int)floorf(fy), a.mh - 1), x0 = min((int)floorf(fx), a.mw - 1);
-      const int y1 = min(y0 + 1, a.mh - 1), x1 = min(x0 + 1, a.mw - 1);
-      const float ly = fminf(fmaxf(fy - y0, 0.f), 1.f), lx = fminf(fmaxf(fx - x0, 0.f), 1.f);
-      v = (1.f - ly) * ((1.f - lx) * map[y0 * a.mw + x0] + lx * map[y0 * a.mw + x1]) +
-          ly * ((1.f - lx) * map[y1 * a.mw + x0] + lx * map[y1 * a.mw + x1]);
+      v = a.img ? a.img[(b * 512 + iy) * 512 + ix] : bilinear512(map, a.mh, a.mw, sh, sw, iy, ix);
       if constexpr (sizeof(T) == 2) v = bf2f(f2bf(v));  // the bf16 path's image is bf16
     }
     s_img[tr * STEM_IMG_PITCH + tc] = v;
@@ -483,7 +490,7 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int py0 = blockIdx.x * STEM_P;
   const int64_t b = blockIdx.y;
-  const float* __restrict__ map = a.map + b * a.mh * a.mw;
+  const float* __restrict__ map = a.img ? nullptr : a.map + b * a.mh * a.mw;
   for (int i = tid; i < 64 * 8; i += 256) {  // [64 co][64 k] bf16 -> pitch 72
     const int co = i >> 3, c8 = (i & 7) * 8;
     *(uint4*)(s_w + co * 72 + c8) = *(const uint4*)((const u16*)a.w + co * 64 + c8);
@@ -494,17 +501,8 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
     const int tr = i / STEM_BPITCH, tc = i - tr * STEM_BPITCH;
     const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
     float v = 0.f;
-    if ((unsigned)iy < 512u && (unsigned)ix < 512u) {
-      float fy = sh * (iy + 0.5f) - 0.5f;
-      fy = fy < 0.f ? 0.f : fy;
-      float fx = sw * (ix + 0.5f) - 0.5f;
-      fx = fx < 0.f ? 0.f : fx;
-      const int y0 = min((int)floorf(fy), a.mh - 1), x0 = min((int)floorf(fx), a.mw - 1);
-      const int y1 = min(y0 + 1, a.mh - 1), x1 = min(x0 + 1, a.mw - 1);
-      const float ly = fminf(fmaxf(fy - y0, 0.f), 1.f), lx = fminf(fmaxf(fx - x0, 0.f), 1.f);
-      v = (1.f - ly) * ((1.f - lx) * map[y0 * a.mw + x0] + lx * map[y0 * a.mw + x1]) +
-          ly * ((1.f - lx) * map[y1 * a.mw + x0] + lx * map[y1 * a.mw + x1]);
-    }
+    if ((unsigned)iy < 512u && (unsigned)ix < 512u)
+      v = a.img ? a.img[(b * 512 + iy) * 512 + ix] : bilinear512(map, a.mh, a.mw, sh, sw, iy, ix);
     s_img[i] = f2bf(v);
   }
   __syncthreads();

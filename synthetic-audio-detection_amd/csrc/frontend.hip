@@ -47,8 +47,9 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+template <typename IT>  // int16_t PCM (scaled by 1/32768, torchaudio.load normalize) or float
 __global__ __launch_bounds__(256) void fe_mel_db_kernel(
-    const int16_t* __restrict__ pcm, int64_t seg_stride, int n_samples, int n_frames, int hop,
+    const IT* __restrict__ pcm, int64_t seg_stride, int n_samples, int n_frames, int hop,
     const float2* __restrict__ tw1024, const float2* __restrict__ tw2048,
     const float* __restrict__ window, const int* __restrict__ mel_start,
     const int* __restrict__ mel_len, const int* __restrict__ mel_off,
@@ -60,7 +61,8 @@ __global__ __launch_bounds__(256) void fe_mel_db_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t seg = blockIdx.y;
-  const int16_t* x = pcm + seg * seg_stride;
+  const IT* x = pcm + seg * seg_stride;
+  const float in_scale = sizeof(IT) == 2 ? (1.0f / 32768.0f) : 1.0f;
   for (int i = tid; i < FE_NC; i += 256) s_tw[i] = tw1024[i];
   for (int i = tid; i <= FE_NC; i += 256) s_tw2[i] = tw2048[i];
   __syncthreads();
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(256) void fe_mel_db_kernel(
             int idx = t * hop + n - pad;
             idx = idx < 0 ? -idx : idx;
             idx = idx >= n_samples ? 2 * (n_samples - 1) - idx : idx;
-            e[q] = (float)x[idx] * (1.0f / 32768.0f) * window[n];
+            e[q] = (float)x[idx] * in_scale * window[n];
           }
           v[b][r] = make_float2(e[0], e[1]);
         }
@@ -343,10 +345,11 @@ extern "C" int sad_frontend_frames(const sad_frontend_plan* p, int32_t* n) {
   return SAD_OK;
 }
 
-extern "C" int sad_frontend_run(const sad_frontend_plan* p, const int16_t* pcm, int64_t n_seg,
-                                int64_t seg_stride, float* out_db, float* out_map, void* stream) {
+template <typename IT>
+static int frontend_run(const sad_frontend_plan* p, const IT* pcm, int64_t n_seg, int64_t seg_stride,
+                        float* out_db, float* out_map, void* stream) {
   SAD_REQUIRE(p, "null plan");
-  SAD_REQUIRE(n_seg >= 0 && n_seg < 65536 * 32, "n_seg out of range");
+  SAD_REQUIRE(n_seg >= 0, "n_seg < 0");
   SAD_REQUIRE(out_map, "out_map is required");
   SAD_REQUIRE(seg_stride >= p->cfg.n_samples, "seg_stride < n_samples");
   if (n_seg == 0) return SAD_OK;
@@ -358,7 +361,7 @@ extern "C" int sad_frontend_run(const sad_frontend_plan* p, const int16_t* pcm, 
   while (done < n_seg) {  // gridDim.y <= 65535
     const int64_t chunk = std::min<int64_t>(65535, n_seg - done);
     const size_t off = (size_t)done * p->cfg.n_mels * p->n_frames;
-    hipLaunchKernelGGL(fe_mel_db_kernel, dim3(n_fb, (unsigned)chunk), dim3(256), 0, s,
+    hipLaunchKernelGGL(fe_mel_db_kernel<IT>, dim3(n_fb, (unsigned)chunk), dim3(256), 0, s,
                        pcm + done * seg_stride, seg_stride, p->cfg.n_samples, p->n_frames,
                        p->cfg.hop_length, p->d_tw1024, p->d_tw2048, p->d_window, p->d_mel_start,
                        p->d_mel_len, p->d_mel_off, p->d_mel_w, p->cfg.n_mels, p->bin_lo, p->bin_hi,
@@ -370,6 +373,16 @@ extern "C" int sad_frontend_run(const sad_frontend_plan* p, const int16_t* pcm, 
     done += chunk;
   }
   return SAD_OK;
+}
+
+extern "C" int sad_frontend_run(const sad_frontend_plan* p, const int16_t* pcm, int64_t n_seg,
+                                int64_t seg_stride, float* out_db, float* out_map, void* stream) {
+  return frontend_run(p, pcm, n_seg, seg_stride, out_db, out_map, stream);
+}
+
+extern "C" int sad_frontend_run_f32(const sad_frontend_plan* p, const float* wav, int64_t n_seg,
+                                    int64_t seg_stride, float* out_db, float* out_map, void* stream) {
+  return frontend_run(p, wav, n_seg, seg_stride, out_db, out_map, stream);
 }
 
 extern "C" int sad_resize_run(const float* map, int64_t n, int32_t h, int32_t w, int32_t oh,

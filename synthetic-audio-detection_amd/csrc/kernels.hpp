@@ -22,7 +22,9 @@ struct ConvArgs {
 };
 
 struct StemArgs {
-  const float* map;      // [B, mh, mw] standardised maps
+  const float* map;      // [B, mh, mw] standardised maps (bilinearly resized in-kernel), or
+  const float* img;      // [B, 512, 512] fp32 image (one channel of the reference's 3 identical
+                         // channels) when non-null
   int mh, mw;
   const void* w;         // [64 co][64 k] folded conv1; bf16: k = ky*8+kx (7x7 in an 8x8 grid),
                          // f32: k = ky*7+kx (zero for k >= 49),

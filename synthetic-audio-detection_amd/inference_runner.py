@@ -1,0 +1,398 @@
+#!/usr/bin/env python3
+"""Drop-in replacement for the reference's ``modular/source/inference_runner.py``
+on MI355X: same module symbols, same CLI flags and defaults, same checkpoint
+and JSON formats; the device work runs on libsad (HIP, gfx950).
+
+Reference map (file:line in modular/source/inference_runner.py):
+  BinaryClassifier            :28-51   -> sub-model parameter holder (base.* / head.*)
+  ModularMultiHeadClassifier  :53-73   -> device engine; forward returns [B, N+1]
+  load_merged_model           :77-123  -> same key mapping / ValueError / sorted indices
+  AudioConfig, SpectrogramConfig :127-142
+  preprocess_waveform         :144-155 -> sad.audio.load (+ resample), mono, zero-pad
+  waveform_to_spectrogram     :157-174 -> fused HIP front end + resize, [1,3,512,512]
+  slice_waveform              :176-190 -> identical host logic
+  interpret_multihead_logits  :194-214 -> identical host logic (torch CPU fp32)
+  main                        :218-353 -> same flow; windows are batched through the
+                                           device front end and the ensemble
+
+Differences (documented in DESIGN.md):
+  * no CPU fallback: ``--device`` must name an MI355X (the reference silently
+    falls back to CPU, :243);
+  * ``pretrained=True`` ImageNet weights (:35) need a network download; a
+    checkpoint missing backbone keys is an error instead of being filled from
+    them;
+  * extra, non-breaking flags: ``--precision {fp32,bf16}`` (default fp32 = the
+    reference's arithmetic; bf16 = throughput mode) and ``--batch-size``
+    (default 128, the reference's mini-batch at :284).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import List
+
+import numpy as np
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if _HERE not in sys.path:
+    sys.path.insert(0, _HERE)
+
+from sad import audio as _audio  # noqa: E402
+from sad import engine as _engine  # noqa: E402
+from sad import weights as _weights  # noqa: E402
+
+
+# 1. Multi-Head Model ---------------------------------------------------------
+class BinaryClassifier:
+    """Sub-model = ResNet backbone (``base.*``, timm keys) + 2-logit head
+    (``head.*``, nn.Sequential indices); index 0 => Real, 1 => Synthetic.
+    Parameters live on the host until a ModularMultiHeadClassifier uploads them."""
+
+    def __init__(self, model_name: str = 'resnet18', init: str = 'random', seed: int = 0):
+        """init='random': deterministic random backbone/head (stand-in for the
+        reference's timm ``pretrained=True`` ImageNet weights, a network
+        download); init='empty': shapes only, for loading a checkpoint."""
+        if model_name != 'resnet18':
+            raise ValueError(f'only resnet18 backbones are supported on the device path (got {model_name!r})')
+        self.model_name = model_name
+        if init == 'random':
+            bb, hd = _weights.backbone_state_dict(seed), _weights.head_state_dict(seed)
+        else:
+            bb, hd = _weights.empty_state_dicts()
+        sd = OrderedDict()
+        for k, v in bb.items():
+            sd[f'base.{k}'] = v
+        for k, v in hd.items():
+            sd[f'head.{k}'] = v
+        self._sd = sd
+
+    def state_dict(self):
+        return OrderedDict((k, v) for k, v in self._sd.items())
+
+    def load_state_dict(self, sd, strict: bool = True):
+        """torch.nn.Module.load_state_dict key semantics (names must match)."""
+        missing = [k for k in self._sd if k not in sd]
+        unexpected = [k for k in sd if k not in self._sd]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f'Error(s) in loading state_dict: missing {missing[:5]}, unexpected {unexpected[:5]}')
+        for k in self._sd:
+            if k in sd:
+                t = torch.as_tensor(sd[k])
+                if tuple(t.shape) != tuple(self._sd[k].shape):
+                    raise RuntimeError(f'size mismatch for {k}: {tuple(t.shape)} vs {tuple(self._sd[k].shape)}')
+                self._sd[k] = t.detach().to('cpu').clone()
+        return missing, unexpected
+
+    def to(self, device):
+        return self
+
+    def eval(self):
+        return self
+
+
+class ModularMultiHeadClassifier:
+    """N sub-models -> [B, N+1] = [syn_1..syn_N, mean_i real_i] (inference_runner.py:53-73),
+    executed by libsad: identical backbones run once, heads + merge in one pass."""
+
+    def __init__(self, sub_models: List[BinaryClassifier], device='cuda', precision: str = 'fp32',
+                 micro_batch: int = 64):
+        self.sub_models = list(sub_models)
+        self.device = torch.device(device)
+        self.precision = precision
+        self.micro_batch = micro_batch
+        self._eng = None
+
+    def state_dict(self):
+        sd = OrderedDict()
+        for i, m in enumerate(self.sub_models):
+            for k, v in m.state_dict().items():
+                sd[f'sub_models.{i}.{k}'] = v
+        return sd
+
+    @property
+    def engine(self) -> _engine.Engine:
+        if self._eng is None:
+            self._eng = _engine.Engine(self.state_dict(), self.device, dtype='bf16' if self.precision == 'bf16'
+                                       else 'fp32', micro_batch=self.micro_batch)
+        return self._eng
+
+    def to(self, device):
+        if torch.device(device) != self.device:
+            self.device = torch.device(device)
+            self._eng = None
+        return self
+
+    def eval(self):
+        return self
+
+    def forward_pcm(self, wav: torch.Tensor) -> torch.Tensor:
+        """[B, 128000] int16 PCM or fp32 waveform -> [B, N+1] merged logits."""
+        return self.engine.forward_pcm(wav.to(self.device).contiguous())[1]
+
+    def forward_maps(self, maps: torch.Tensor) -> torch.Tensor:
+        return self.engine.forward_maps(maps.to(self.device).contiguous())[1]
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        """x: [B, 3, 512, 512] spectrogram images (the reference's model input)."""
+        x = x.to(self.device, torch.float32)
+        if x.dim() != 4 or x.shape[1] != 3 or x.shape[2:] != (512, 512):
+            raise ValueError(f'expected [B,3,512,512], got {tuple(x.shape)}')
+        if not (torch.equal(x[:, 0], x[:, 1]) and torch.equal(x[:, 0], x[:, 2])):
+            raise NotImplementedError('the device stem folds the 3 identical spectrogram channels '
+                                      '(inference_runner.py:173); distinct channels are not supported')
+        img = x[:, 0].contiguous()
+        eng = self.engine
+        feats = [bb.forward_images(img) for bb in eng.backbones]
+        return eng.heads(feats)[1]
+
+    forward = __call__
+
+
+# 2. Loading the Merged Model from .pth (with metadata) -----------------------
+def load_merged_model(merged_path: str, device: torch.device, backbone_name='resnet18', precision: str = 'fp32'):
+    """inference_runner.py:77-123.  Returns (model, metadata)."""
+    state = torch.load(merged_path, map_location='cpu', weights_only=True)
+    sd = state['state_dict']
+    metadata = state.get('metadata', None)
+    if not metadata or 'class_names' not in metadata:
+        raise ValueError('Merged model checkpoint does not contain metadata for class names!')
+    submodel_indices = set()
+    for k in sd.keys():
+        parts = k.split('.')
+        if len(parts) >= 3 and parts[0] == 'sub_models':
+            try:
+                submodel_indices.add(int(parts[1]))
+            except ValueError:
+                pass
+    submodel_indices = sorted(submodel_indices)
+    print(f'Found {len(submodel_indices)} sub-model(s): {submodel_indices}')
+    sub_models = []
+    for idx in submodel_indices:
+        sm = BinaryClassifier(model_name=backbone_name, init='empty')
+        local_sd = {}
+        missing = []
+        for param_key in sm.state_dict().keys():
+            big_key = f'sub_models.{idx}.' + param_key
+            if big_key in sd:
+                local_sd[param_key] = sd[big_key]
+            elif not param_key.endswith('num_batches_tracked'):
+                missing.append(param_key)
+        if missing:
+            # The reference fills these from timm's ImageNet weights (pretrained=True, :35),
+            # a network download that is unavailable offline.
+            raise KeyError(f'sub-model {idx} lacks {len(missing)} tensors (e.g. {missing[0]}); '
+                           'pretrained ImageNet defaults are not available offline')
+        sm.load_state_dict(local_sd, strict=False)
+        sub_models.append(sm)
+    final_model = ModularMultiHeadClassifier(sub_models, device, precision)
+    # Quick test (reference :119-122): build the device plans, one dummy forward.
+    dummy = final_model.forward_maps(torch.zeros(2, 128, 251))
+    print('Rebuilt merged model => dummy output shape:', torch.Size([2, dummy.shape[1]]))
+    return final_model, metadata
+
+
+# 3. Overlapping Window + Spectrogram Logic -----------------------------------
+@dataclass
+class AudioConfig:
+    sample_rate: int = 32000
+    window_size: float = 4.0  # seconds
+    overlap: float = 0.85     # fraction overlap
+    silence_threshold: float = 1e-4
+
+
+@dataclass
+class SpectrogramConfig:
+    n_fft: int = 2048
+    hop_length: int = 512
+    n_mels: int = 128
+    f_min: int = 20
+    f_max: int = 12000
+    top_db: int = 80
+    norm: str = 'slaney'
+
+
+def preprocess_waveform(path: str, cfg: AudioConfig):
+    """inference_runner.py:144-155 -> (mono fp32 [T], sr)."""
+    wf, sr = _audio.load(path)
+    wf = wf.mean(dim=0)
+    if sr != cfg.sample_rate:
+        wf = _audio.resample(wf, sr, cfg.sample_rate)
+        sr = cfg.sample_rate
+    needed = int(cfg.window_size * sr)
+    if wf.shape[0] < needed:
+        temp = torch.zeros(needed)
+        temp[:wf.shape[0]] = wf
+        wf = temp
+    return wf, sr
+
+
+_FE_CACHE = {}
+
+
+def _frontend(device, spec_cfg: SpectrogramConfig, n_samples: int, sr: int):
+    key = (str(device), spec_cfg.n_fft, spec_cfg.hop_length, spec_cfg.n_mels, spec_cfg.f_min, spec_cfg.f_max,
+           spec_cfg.top_db, spec_cfg.norm, n_samples, sr)
+    if key not in _FE_CACHE:
+        _FE_CACHE[key] = _engine.FrontEnd(device, norm=spec_cfg.norm, n_samples=n_samples, sample_rate=sr,
+                                          n_fft=spec_cfg.n_fft, hop=spec_cfg.hop_length, n_mels=spec_cfg.n_mels,
+                                          f_min=float(spec_cfg.f_min), f_max=float(spec_cfg.f_max),
+                                          top_db=spec_cfg.top_db)
+    return _FE_CACHE[key]
+
+
+def waveform_to_spectrogram(waveform: torch.Tensor, sr: int, spec_cfg: SpectrogramConfig, device='cuda'):
+    """inference_runner.py:157-174 -> [1, 3, 512, 512] fp32 on the device."""
+    dev = _engine._dev(device)
+    wf = waveform.to(dev, torch.float32).reshape(1, -1).contiguous()
+    fe = _frontend(dev, spec_cfg, wf.shape[1], sr)
+    m = fe(wf)
+    img = _engine.resize(m, (512, 512))
+    return img.unsqueeze(1).repeat(1, 3, 1, 1)
+
+
+def slice_waveform(wf: torch.Tensor, sr: int, cfg: AudioConfig):
+    """inference_runner.py:176-190: list of window views + start times (s)."""
+    window_samples = int(cfg.window_size * sr)
+    hop_samples = int((1 - cfg.overlap) * window_samples)
+    chunks, timestamps = [], []
+    for start_idx in range(0, wf.shape[0] - window_samples + 1, hop_samples):
+        piece = wf[start_idx:start_idx + window_samples]
+        if piece.abs().max() < cfg.silence_threshold:
+            continue
+        chunks.append(piece)
+        timestamps.append(start_idx / sr)
+    return chunks, timestamps
+
+
+# 4. Probability Interpretation (Using Metadata) -------------------------------
+def interpret_multihead_logits(logits: torch.Tensor, threshold=0.5, synthetic_names: List[str] = None,
+                               real_name: str = 'Real'):
+    """inference_runner.py:194-214 (host, fp32)."""
+    s = torch.sigmoid(logits.detach().to('cpu', torch.float32))
+    n = s.shape[0] - 1
+    syn_probs = s[:n]
+    real_prob = s[-1]
+    if real_prob >= threshold and (syn_probs < threshold).all():
+        label = real_name
+    else:
+        idx = int(torch.argmax(syn_probs).item())
+        if synthetic_names and idx < len(synthetic_names):
+            label = synthetic_names[idx]
+        else:
+            label = f'Synthetic_{idx + 1}'
+    return label, s.numpy()
+
+
+def summarize(filename, outputs, timestamps, threshold, synthetic_names, real_name, smooth, window_size):
+    """inference_runner.py:292-349: decisions, optional smoothing, percentages, segments."""
+    from scipy.ndimage import gaussian_filter1d
+    raw_labels, raw_probs = [], []
+    for row in outputs:
+        label, s = interpret_multihead_logits(row, threshold=threshold, synthetic_names=synthetic_names,
+                                              real_name=real_name)
+        raw_labels.append(label)
+        raw_probs.append(s)
+    if smooth:
+        raw_probs_arr = np.array(raw_probs)
+        for dim in range(raw_probs_arr.shape[1]):
+            raw_probs_arr[:, dim] = gaussian_filter1d(raw_probs_arr[:, dim], sigma=2)
+        for i in range(raw_probs_arr.shape[0]):
+            row_sum = raw_probs_arr[i].sum()
+            if row_sum > 0:
+                raw_probs_arr[i] /= row_sum
+        smoothed_labels = []
+        for i in range(raw_probs_arr.shape[0]):
+            real_p = raw_probs_arr[i, -1]
+            syn_p = raw_probs_arr[i, :-1]
+            if real_p >= threshold and (syn_p < threshold).all():
+                label2 = real_name
+            else:
+                idx = int(syn_p.argmax())
+                label2 = synthetic_names[idx] if idx < len(synthetic_names) else f'Synthetic_{idx + 1}'
+            smoothed_labels.append(label2)
+        raw_labels = smoothed_labels
+        raw_probs = raw_probs_arr.tolist()
+    final_probs_arr = np.mean(raw_probs, axis=0)
+    prob_dict = {}
+    n_syn = len(final_probs_arr) - 1
+    for i in range(n_syn):
+        name = synthetic_names[i] if i < len(synthetic_names) else f'Synthetic_{i + 1}'
+        prob_dict[name] = float(final_probs_arr[i] * 100)
+    prob_dict[real_name] = float(final_probs_arr[-1] * 100)
+    segments = [{'start_sec': timestamps[i], 'end_sec': timestamps[i] + window_size, 'label': lbl}
+                for i, lbl in enumerate(raw_labels)]
+    return {'filename': filename, 'segments': segments, 'percentages': prob_dict}
+
+
+def run_windows(model: ModularMultiHeadClassifier, chunks, sr: int, spec_cfg: SpectrogramConfig,
+                batch_size: int = 128) -> torch.Tensor:
+    """All windows -> [n, N+1] merged logits (fp32, host): device front end +
+    ensemble, `batch_size` windows per launch (the reference's mini-batch, :284)."""
+    dev = model.device
+    fe = _frontend(dev, spec_cfg, chunks[0].shape[0], sr)
+    outs = []
+    for start in range(0, len(chunks), batch_size):
+        wav = torch.stack(chunks[start:start + batch_size]).to(dev, torch.float32).contiguous()
+        outs.append(model.forward_maps(fe(wav)).cpu())
+    return torch.cat(outs)
+
+
+# 5. Main Inference Logic -------------------------------------------------------
+def main(argv=None):
+    parser = argparse.ArgumentParser(
+        description='Multi-head inference with overlapping windows using metadata from the merged model.')
+    parser.add_argument('--merged-model', type=str, required=True, help='Path to merged .pth')
+    parser.add_argument('--audio', type=str, required=True, help='Path to WAV file')
+    parser.add_argument('--threshold', type=float, default=0.5, help='Threshold for deciding Real vs Synthetic')
+    parser.add_argument('--device', type=str, default='cuda')
+    parser.add_argument('--confidence-threshold', type=float, default=0.45, help='Confidence threshold for segments.')
+    parser.add_argument('--smooth', action='store_true', help='Apply smoothing across windows.')
+    parser.add_argument('--output-json', type=str, default='results.json')
+    parser.add_argument('--precision', choices=['fp32', 'bf16'], default='fp32',
+                        help='device arithmetic: fp32 (reference numerics) or bf16 (throughput)')
+    parser.add_argument('--batch-size', type=int, default=128, help='windows per device launch')
+    args = parser.parse_args(argv)
+
+    seed = 9
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    device = _engine._dev(args.device)
+
+    model, metadata = load_merged_model(args.merged_model, device, precision=args.precision)
+    class_names = metadata['class_names']
+    synthetic_names = class_names[:-1]
+    real_name = class_names[-1]
+    print('Using metadata names:')
+    print('Synthetic names:', synthetic_names)
+    print('Real name:', real_name)
+
+    audio_cfg = AudioConfig(sample_rate=32000, window_size=4.0, overlap=0.0, silence_threshold=1e-3)
+    spec_cfg = SpectrogramConfig(n_fft=2048, hop_length=512, n_mels=128, f_min=20, f_max=12000, top_db=80,
+                                 norm='slaney')
+    wf, sr = preprocess_waveform(args.audio, audio_cfg)
+    chunks, timestamps = slice_waveform(wf, sr, audio_cfg)
+    if not chunks:
+        print('No valid audio chunks found (all below silence threshold). Exiting.')
+        out = {'filename': args.audio, 'segments': [], 'percentages': {}}
+        with open(args.output_json, 'w', encoding='utf-8') as f:
+            json.dump(out, f, indent=4)
+        return out
+    outputs = run_windows(model, chunks, sr, spec_cfg, args.batch_size)
+    out_json = summarize(args.audio, outputs, timestamps, args.threshold, synthetic_names, real_name,
+                         args.smooth, audio_cfg.window_size)
+    with open(args.output_json, 'w', encoding='utf-8') as f:
+        json.dump(out_json, f, indent=4)
+    print('Wrote results to', args.output_json)
+    print(json.dumps(out_json, indent=4))
+    return out_json
+
+
+if __name__ == '__main__':
+    main()

@@ -43,11 +43,13 @@ SIGNATURES = {
     'sad_frontend_plan_destroy': (ctypes.c_int, [P]),
     'sad_frontend_frames': (ctypes.c_int, [P, ctypes.POINTER(I32)]),
     'sad_frontend_run': (ctypes.c_int, [P, P, I64, I64, P, P, P]),
+    'sad_frontend_run_f32': (ctypes.c_int, [P, P, I64, I64, P, P, P]),
     'sad_resize_run': (ctypes.c_int, [P, I64, I32, I32, I32, I32, I32, P, P]),
     'sad_backbone_plan_create': (ctypes.c_int, [FPP, I32, I32, I32, I32, ctypes.POINTER(P)]),
     'sad_backbone_plan_destroy': (ctypes.c_int, [P]),
     'sad_backbone_workspace_size': (ctypes.c_int, [P, I64, ctypes.POINTER(SZ)]),
     'sad_backbone_run': (ctypes.c_int, [P, P, I64, I64, P, P, SZ, P]),
+    'sad_backbone_run_img': (ctypes.c_int, [P, P, I64, I64, P, P, SZ, P]),
     'sad_backbone_stem_run': (ctypes.c_int, [P, P, I64, P, P]),
     'sad_backbone_run_debug': (ctypes.c_int, [P, P, I64, P, P, P, SZ, P]),
     'sad_heads_plan_create': (ctypes.c_int, [FPP, I32, ctypes.POINTER(I32), I32, ctypes.POINTER(P)]),

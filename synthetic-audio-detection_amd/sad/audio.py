@@ -1,0 +1,131 @@
+"""Host-side audio ingestion: WAV decode and torchaudio-compatible resampling.
+
+Replaces ``torchaudio.load`` and ``torchaudio.transforms.Resample`` as used by
+``preprocess_waveform`` (inference_runner.py:144-155) and the trainer dataset
+(submodel_trainer.py:143,150-153).  torchaudio is not available in this image;
+these are restatements of its documented behaviour:
+
+* ``load(path)`` -> (float32 [channels, frames], sample_rate), integer PCM
+  scaled by 1/2^(bits-1) (torchaudio ``normalize=True``), float WAV as is.
+  Supports RIFF/WAVE PCM 8/16/24/32-bit and IEEE float 32/64 (incl.
+  WAVE_FORMAT_EXTENSIBLE).
+* ``resample(wf, orig, new)`` -> torchaudio.functional.resample with its
+  defaults (sinc_interp_hann, lowpass_filter_width=6, rolloff=0.99): windowed
+  sinc kernel built in float64, cast to float32, applied as a strided conv1d.
+
+Host (CPU) work in the reference too: it happens once per file, before the
+device hot path.
+"""
+from __future__ import annotations
+
+import math
+import struct
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def _read_chunks(data: bytes):
+    if data[:4] != b'RIFF' or data[8:12] != b'WAVE':
+        raise ValueError('not a RIFF/WAVE file')
+    pos, fmt, payload = 12, None, None
+    while pos + 8 <= len(data):
+        cid, size = data[pos:pos + 4], struct.unpack('<I', data[pos + 4:pos + 8])[0]
+        body = data[pos + 8:pos + 8 + size]
+        if cid == b'fmt ':
+            fmt = body
+        elif cid == b'data':
+            payload = body
+        pos += 8 + size + (size & 1)
+    if fmt is None or payload is None:
+        raise ValueError('WAV file lacks fmt/data chunks')
+    return fmt, payload
+
+
+def load(path: str):
+    """torchaudio.load(path) for WAV files -> (Tensor[C, T] float32, sample_rate)."""
+    with open(path, 'rb') as f:
+        data = f.read()
+    fmt, payload = _read_chunks(data)
+    tag, ch, sr, _, _, bits = struct.unpack('<HHIIHH', fmt[:16])
+    if tag == 0xFFFE and len(fmt) >= 26:  # WAVE_FORMAT_EXTENSIBLE: sub-format GUID's first 2 bytes
+        tag = struct.unpack('<H', fmt[24:26])[0]
+    width = bits // 8
+    n = len(payload) // (width * ch)
+    raw = payload[:n * width * ch]
+    if tag == 1:  # PCM
+        if bits == 8:
+            x = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128.0) / 128.0
+        elif bits == 16:
+            x = np.frombuffer(raw, '<i2').astype(np.float32) / 32768.0
+        elif bits == 24:
+            b = np.frombuffer(raw, np.uint8).reshape(-1, 3).astype(np.int32)
+            v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+            v = np.where(v >= 1 << 23, v - (1 << 24), v)
+            x = v.astype(np.float32) / float(1 << 23)
+        elif bits == 32:
+            x = (np.frombuffer(raw, '<i4').astype(np.float64) / float(1 << 31)).astype(np.float32)
+        else:
+            raise ValueError(f'unsupported PCM width {bits}')
+    elif tag == 3:  # IEEE float
+        x = np.frombuffer(raw, '<f4' if bits == 32 else '<f8').astype(np.float32)
+    else:
+        raise ValueError(f'unsupported WAV format tag {tag:#x}')
+    return torch.from_numpy(x.reshape(n, ch).T.copy()), sr
+
+
+def load_pcm16_mono(path: str):
+    """Fast path for the common case (mono 16-bit PCM): (int16 ndarray [T], sr) or None."""
+    with open(path, 'rb') as f:
+        data = f.read()
+    fmt, payload = _read_chunks(data)
+    tag, ch, sr, _, _, bits = struct.unpack('<HHIIHH', fmt[:16])
+    if tag != 1 or ch != 1 or bits != 16:
+        return None
+    return np.frombuffer(payload[:len(payload) // 2 * 2], '<i2').copy(), sr
+
+
+def save_pcm16(path: str, pcm: np.ndarray, sr: int = 32000):
+    import wave
+    pcm = np.atleast_2d(pcm)
+    with wave.open(path, 'wb') as w:
+        w.setnchannels(pcm.shape[0])
+        w.setsampwidth(2)
+        w.setframerate(sr)
+        w.writeframes(np.ascontiguousarray(pcm.T).astype('<i2').tobytes())
+
+
+def _sinc_resample_kernel(orig: int, new: int, gcd: int, lowpass_filter_width: int = 6, rolloff: float = 0.99,
+                          device=None):
+    orig //= gcd
+    new //= gcd
+    base = min(orig, new) * rolloff
+    width = math.ceil(lowpass_filter_width * orig / base)
+    idx = torch.arange(-width, width + orig, dtype=torch.float64, device=device)[None, None] / orig
+    t = torch.arange(0, -new, -1, device=device)[:, None, None] / new + idx
+    t = t * base
+    t = t.clamp_(-lowpass_filter_width, lowpass_filter_width)
+    window = torch.cos(t * math.pi / lowpass_filter_width / 2) ** 2
+    t = t * math.pi
+    scale = base / orig
+    kernels = torch.where(t == 0, torch.tensor(1.0).to(t), t.sin() / t)
+    kernels = kernels * window * scale
+    return kernels.to(torch.float32), width
+
+
+def resample(wf: torch.Tensor, orig_freq: int, new_freq: int) -> torch.Tensor:
+    """torchaudio.functional.resample(wf, orig, new) with default arguments."""
+    if orig_freq == new_freq:
+        return wf
+    gcd = math.gcd(int(orig_freq), int(new_freq))
+    kernel, width = _sinc_resample_kernel(int(orig_freq), int(new_freq), gcd, device=wf.device)
+    o, n = int(orig_freq) // gcd, int(new_freq) // gcd
+    shape = wf.shape
+    x = wf.reshape(-1, shape[-1])
+    length = x.shape[1]
+    x = F.pad(x, (width, width + o))
+    y = F.conv1d(x[:, None], kernel, stride=o)
+    y = y.transpose(1, 2).reshape(x.shape[0], -1)
+    target = int(math.ceil(n * length / o))
+    return y[..., :target].reshape(shape[:-1] + (-1,))

@@ -58,17 +58,19 @@ class FrontEnd:
         _lib.call('sad_frontend_frames', self._plan, _lib.ctypes.byref(nf))
         self.n_frames, self.n_mels, self.n_samples = nf.value, n_mels, n_samples
 
-    def __call__(self, pcm: torch.Tensor, want_db: bool = False):
-        """pcm [n, >=n_samples] int16 on device -> map [n, n_mels, frames] fp32
-        (and the clamped dB map if want_db)."""
-        assert pcm.dtype == torch.int16 and pcm.device == self.device and pcm.dim() == 2
+    def __call__(self, pcm: torch.Tensor, want_db: bool = False, out: torch.Tensor | None = None):
+        """pcm [n, >=n_samples] int16 (or fp32 waveform in [-1,1)) on device ->
+        map [n, n_mels, frames] fp32 (and the clamped dB map if want_db)."""
+        assert pcm.dtype in (torch.int16, torch.float32) and pcm.device == self.device and pcm.dim() == 2
         assert pcm.stride(1) == 1 and pcm.shape[1] >= self.n_samples
         n = pcm.shape[0]
-        out = torch.empty(n, self.n_mels, self.n_frames, device=self.device, dtype=torch.float32)
+        if out is None:
+            out = torch.empty(n, self.n_mels, self.n_frames, device=self.device, dtype=torch.float32)
         db = torch.empty_like(out) if want_db else None
+        fn = 'sad_frontend_run' if pcm.dtype == torch.int16 else 'sad_frontend_run_f32'
         with torch.cuda.device(self.device):
-            _lib.call('sad_frontend_run', self._plan, _lib.ptr(pcm), n, pcm.stride(0), _lib.ptr(db),
-                      _lib.ptr(out), _lib.stream_handle(self.device))
+            _lib.call(fn, self._plan, _lib.ptr(pcm), n, pcm.stride(0), _lib.ptr(db), _lib.ptr(out),
+                      _lib.stream_handle(self.device))
         return (out, db) if want_db else out
 
     def __del__(self):
@@ -131,6 +133,18 @@ class Backbone:
         ws = self.workspace(mb)
         with torch.cuda.device(self.device):
             _lib.call('sad_backbone_run', self._plan, _lib.ptr(maps), B, mb, _lib.ptr(feats), _lib.ptr(ws),
+                      ws.numel(), _lib.stream_handle(self.device))
+        return feats
+
+    def forward_images(self, img: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """img [B,512,512] fp32 (one channel of the reference's identical three) -> feats."""
+        assert img.dtype == torch.float32 and img.shape[1:] == (512, 512) and img.is_contiguous()
+        B = img.shape[0]
+        feats = out if out is not None else torch.empty(B, 512, device=self.device, dtype=torch.float32)
+        mb = max(1, min(self.micro_batch, B))
+        ws = self.workspace(mb)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_backbone_run_img', self._plan, _lib.ptr(img), B, mb, _lib.ptr(feats), _lib.ptr(ws),
                       ws.numel(), _lib.stream_handle(self.device))
         return feats
 

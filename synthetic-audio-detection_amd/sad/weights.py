@@ -93,6 +93,30 @@ def head_state_dict(seed: int) -> "OrderedDict[str, torch.Tensor]":
     return sd
 
 
+def empty_state_dicts():
+    """(backbone, head) state dicts with the right keys/shapes and placeholder
+    values (zeros; BN var = 1) -- the cheap skeleton a checkpoint is loaded into."""
+    bb = OrderedDict()
+    for key, shape, kind in backbone_param_shapes():
+        if kind == 'conv':
+            bb[f'{key}.weight'] = torch.zeros(shape)
+        else:
+            c = shape[0]
+            bb[f'{key}.weight'], bb[f'{key}.bias'] = torch.ones(c), torch.zeros(c)
+            bb[f'{key}.running_mean'], bb[f'{key}.running_var'] = torch.zeros(c), torch.ones(c)
+            bb[f'{key}.num_batches_tracked'] = torch.tensor(0, dtype=torch.long)
+    hd = OrderedDict()
+    for idx, kind, shape in HEAD_LAYOUT:
+        if kind == 'linear':
+            hd[f'{idx}.weight'], hd[f'{idx}.bias'] = torch.zeros(shape), torch.zeros(shape[0])
+        else:
+            c = shape[0]
+            hd[f'{idx}.weight'], hd[f'{idx}.bias'] = torch.ones(c), torch.zeros(c)
+            hd[f'{idx}.running_mean'], hd[f'{idx}.running_var'] = torch.zeros(c), torch.ones(c)
+            hd[f'{idx}.num_batches_tracked'] = torch.tensor(0, dtype=torch.long)
+    return bb, hd
+
+
 def merged_state_dict(seed: int = 0, n_heads: int = 6, distinct_backbones: bool = False,
                       bn_stats: dict | None = None) -> "OrderedDict[str, torch.Tensor]":
     """Merged checkpoint state dict.  Sub-model i uses backbone seed
