@@ -1,6 +1,7 @@
 // api.hip -- C ABI of libsad.so: runtime, backbone and heads plans.
 // Declarations and the reference interfaces each entry replaces: include/sad.h.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -45,13 +46,24 @@ struct DevConv {
 
 using namespace sad;
 
+struct DevBlock {           // one BasicBlock on the block-conv path
+  int cin, cout, stride;
+  void* w1 = nullptr;        // conv1: [cout][9*cin]
+  float* b1 = nullptr;
+  void* w2 = nullptr;        // conv2 + shortcut: [cout][9*cout + cin_sc] (identity or downsample)
+  float* b2 = nullptr;
+  int cin_sc;
+};
+
 struct sad_backbone_plan {
   int dtype;
   int mh, mw;
   int device;
+  bool block_path;           // true: persistent block-conv kernels (shortcut in GEMM)
   void* stem_w = nullptr;
   float* stem_b = nullptr;
-  std::vector<DevConv> convs;  // index 1.. of the spec table
+  std::vector<DevConv> convs;  // index 1.. of the spec table (igemm path)
+  std::vector<DevBlock> blocks;
 };
 
 struct sad_heads_plan {
@@ -161,6 +173,57 @@ extern "C" int sad_backbone_plan_create(const float* const* params, int32_t n_pa
     if ((rc = upload((void**)&d.bias, bf))) return rc;
     p->convs.push_back(d);
   }
+  // block path: conv2 and the shortcut (identity or folded downsample) share one
+  // GEMM with a concatenated K axis; biases add.
+  {
+    const char* env = getenv("SAD_BACKBONE_PATH");
+    p->block_path = !(env && strcmp(env, "igemm") == 0);
+    size_t ci = 1;
+    int inp = 64;
+    const int planes[4] = {64, 128, 256, 512};
+    for (int li = 0; li < 4; ++li) {
+      for (int b = 0; b < 2; ++b) {
+        const size_t i1 = ci++, i2 = ci++;
+        const bool has_ds = (b == 0 && li > 0);
+        const size_t ids = has_ds ? ci++ : 0;
+        const int co = planes[li];
+        DevBlock blk;
+        blk.cin = inp;
+        blk.cout = co;
+        blk.stride = has_ds ? 2 : 1;
+        blk.cin_sc = inp;
+        std::vector<double> sc1, sh1, sc2, sh2, scd, shd;
+        fold_bn(params[i1 * 5 + 1], params[i1 * 5 + 2], params[i1 * 5 + 3], params[i1 * 5 + 4], co, sc1, sh1);
+        fold_bn(params[i2 * 5 + 1], params[i2 * 5 + 2], params[i2 * 5 + 3], params[i2 * 5 + 4], co, sc2, sh2);
+        if (has_ds) fold_bn(params[ids * 5 + 1], params[ids * 5 + 2], params[ids * 5 + 3], params[ids * 5 + 4], co, scd, shd);
+        const int k1 = 9 * inp, k2 = 9 * co + inp;
+        std::vector<double> w1((size_t)co * k1), w2((size_t)co * k2, 0.0), b2(co);
+        const float* W1 = params[i1 * 5];
+        const float* W2 = params[i2 * 5];
+        for (int o = 0; o < co; ++o) {
+          for (int c = 0; c < inp; ++c)
+            for (int t = 0; t < 9; ++t) w1[(size_t)o * k1 + t * inp + c] = (double)W1[((size_t)o * inp + c) * 9 + t] * sc1[o];
+          for (int c = 0; c < co; ++c)
+            for (int t = 0; t < 9; ++t) w2[(size_t)o * k2 + t * co + c] = (double)W2[((size_t)o * co + c) * 9 + t] * sc2[o];
+          if (has_ds) {
+            const float* Wd = params[ids * 5];
+            for (int c = 0; c < inp; ++c) w2[(size_t)o * k2 + 9 * co + c] = (double)Wd[(size_t)o * inp + c] * scd[o];
+            b2[o] = sh2[o] + shd[o];
+          } else {
+            w2[(size_t)o * k2 + 9 * co + o] = 1.0;  // identity shortcut (exact in bf16)
+            b2[o] = sh2[o];
+          }
+        }
+        if ((rc = upload_typed(&blk.w1, w1, dtype))) return rc;
+        if ((rc = upload_typed(&blk.w2, w2, dtype))) return rc;
+        std::vector<float> b1f(sh1.begin(), sh1.end()), b2f(b2.begin(), b2.end());
+        if ((rc = upload((void**)&blk.b1, b1f))) return rc;
+        if ((rc = upload((void**)&blk.b2, b2f))) return rc;
+        p->blocks.push_back(blk);
+        inp = co;
+      }
+    }
+  }
   *out = p;
   return SAD_OK;
 }
@@ -172,6 +235,12 @@ extern "C" int sad_backbone_plan_destroy(sad_backbone_plan* p) {
   for (auto& c : p->convs) {
     (void)hipFree(c.w);
     (void)hipFree(c.bias);
+  }
+  for (auto& b : p->blocks) {
+    (void)hipFree(b.w1);
+    (void)hipFree(b.b1);
+    (void)hipFree(b.w2);
+    (void)hipFree(b.b2);
   }
   delete p;
   return SAD_OK;
@@ -200,8 +269,49 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
   int rc = launch_stem(st, p->dtype, s);
   if (rc) return rc;
   int H = 128, C = 64;
+  if (p->block_path) {
+    for (const DevBlock& blk : p->blocks) {
+      const int Ho = H / blk.stride;
+      BlockConvArgs a{};
+      a.in0 = bufA;
+      a.in0_pstride = C;
+      a.N = (int)mb;
+      a.H = a.W = H;
+      a.Cin = C;
+      a.KH = a.KW = 3;
+      a.stride = blk.stride;
+      a.pad = 1;
+      a.wt = blk.w1;
+      a.bias = blk.b1;
+      a.out = bufT;
+      a.out_pstride = blk.cout;
+      a.Ho = a.Wo = Ho;
+      a.Cout = blk.cout;
+      a.relu = 1;
+      a.M = mb * Ho * Ho;
+      if ((rc = launch_block_conv(a, p->dtype, s))) return rc;
+      BlockConvArgs b2 = a;
+      b2.in0 = bufT;
+      b2.in0_pstride = blk.cout;
+      b2.H = b2.W = Ho;
+      b2.Cin = blk.cout;
+      b2.stride = 1;
+      b2.in1 = bufA;
+      b2.in1_pstride = C;
+      b2.H1 = b2.W1 = H;
+      b2.Cin1 = C;
+      b2.ss1 = blk.stride;
+      b2.wt = blk.w2;
+      b2.bias = blk.b2;
+      b2.out = bufB;
+      if ((rc = launch_block_conv(b2, p->dtype, s))) return rc;
+      std::swap(bufA, bufB);
+      H = Ho;
+      C = blk.cout;
+    }
+  }
   size_t ci = 0;
-  for (int li = 0; li < 4; ++li) {
+  for (int li = 0; li < 4 && !p->block_path; ++li) {
     for (int b = 0; b < 2; ++b) {
       const DevConv& c1 = p->convs[ci++];
       const DevConv& c2 = p->convs[ci++];
@@ -501,4 +611,40 @@ extern "C" int sad_conv2d_run(const void* in, int64_t N, int32_t H, int32_t W, i
   a.relu = relu;
   a.M = N * a.Ho * a.Wo;
   return launch_conv(a, dtype, (hipStream_t)stream, variant);
+}
+
+extern "C" int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* in1,
+                                  int32_t H1, int32_t W1, int32_t Cin1, int32_t ss1, const void* wt,
+                                  const float* bias, void* out, int32_t Cout, int32_t k, int32_t stride,
+                                  int32_t pad, int32_t relu, int32_t dtype, int32_t variant, void* stream) {
+  SAD_REQUIRE(in0 && wt && bias && out, "null tensor");
+  SAD_REQUIRE(N >= 0 && H > 0 && W > 0 && k > 0 && stride > 0 && pad >= 0, "bad shape");
+  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
+  BlockConvArgs a{};
+  a.in0 = in0;
+  a.in0_pstride = Cin;
+  a.N = (int)N;
+  a.H = H;
+  a.W = W;
+  a.Cin = Cin;
+  a.KH = a.KW = k;
+  a.stride = stride;
+  a.pad = pad;
+  a.in1 = in1;
+  a.in1_pstride = Cin1;
+  a.H1 = H1;
+  a.W1 = W1;
+  a.Cin1 = in1 ? Cin1 : 0;
+  a.ss1 = ss1;
+  a.wt = wt;
+  a.bias = bias;
+  a.out = out;
+  a.out_pstride = Cout;
+  a.Ho = (H + 2 * pad - k) / stride + 1;
+  a.Wo = (W + 2 * pad - k) / stride + 1;
+  if (in1) SAD_REQUIRE((a.Ho - 1) * ss1 < H1 && (a.Wo - 1) * ss1 < W1, "shortcut source too small");
+  a.Cout = Cout;
+  a.relu = relu;
+  a.M = N * a.Ho * a.Wo;
+  return launch_block_conv(a, dtype, (hipStream_t)stream, variant);
 }

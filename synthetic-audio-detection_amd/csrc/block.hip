@@ -1,0 +1,305 @@
+// block.hip -- persistent implicit-GEMM conv with the shortcut inside the GEMM.
+//
+// Replaces one timm BasicBlock half (conv -> bn [-> + shortcut] -> relu,
+// inference_runner.py:49-51 via timm resnet18) as ONE GEMM over a concatenated
+// K axis:
+//   out[px, co] = act( sum_{k0} X0[px; k0] W0[co, k0]          3x3 conv, BN folded
+//                    + sum_{k1} X1[px*ss1; k1] W1[co, k1]      shortcut (optional)
+//                    + bias[co] )
+// The shortcut is either the identity (W1 = I, exact in bf16: the residual add
+// becomes MFMA work, +Cin/(9 Cin) MACs) or the 1x1/2 downsample conv + its BN
+// (W1 = folded downsample weights).  So a block needs two launches instead of
+// three, and no epilogue ever reads the residual tensor.
+//
+// Structure (gfx950):
+//  * operands swapped: C^T[co, px] = W . X^T, so each lane's 16x16 MFMA
+//    accumulator holds 4 CONSECUTIVE output channels of one pixel -> the
+//    epilogue is register-only (bias, ReLU, bf16 pack, one 8-B store per
+//    16x16 tile per lane): no LDS staging, no barrier.
+//  * persistent workgroups: grid = CUs x occupancy; workgroup w owns channel
+//    tile w % n_tc (so its weights' DMA offsets and its bias registers are
+//    fixed) and a contiguous run of pixel tiles (neighbouring tiles share input
+//    rows through the XCD's L2).  The LDS-DMA ring (S stages, inline-asm
+//    buffer_load...lds, counted vmcnt) runs continuously ACROSS tile
+//    boundaries, so a tile's first K-steps are in flight while the previous
+//    tile finishes and stores.
+//  * one K-step = one filter tap (or shortcut chunk) x 128 B of channels
+//    (64 bf16 / 32 f32), 8 x 16-B chunks per pixel row, XOR-swizzled through
+//    the DMA source address (LDS-DMA writes lane-linearly).
+#include "common.hpp"
+#include "igemm.hpp"
+#include "kernels.hpp"
+
+namespace sad {
+
+// WC x WP waves; each wave owns (16*TC) channels x (16*TP) pixels (TC, TP 16x16
+// MFMA tiles); OCC = workgroups per CU the LDS budget admits.
+template <int WC, int WP, int TC, int TP, int S>
+constexpr int block_smem_bytes() {
+  return S * (16 * TP * WP + 16 * TC * WC) * 128;
+}
+
+template <typename T, int WC, int WP, int TC, int TP, int S, int OCC>
+__global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_kernel(BlockConvArgs a) {
+  static_assert(S == 2 || S == 3, "ring depth");
+  constexpr int NW = WC * WP;
+  constexpr int BC = 16 * TC * WC, BP = 16 * TP * WP;  // channels x pixels per tile
+  constexpr int ES = sizeof(T);
+  constexpr int STAGE = (BP + BC) * 128;     // rows [0,BP): pixels, [BP,BP+BC): weights
+  constexpr int QP = BP / 8 / NW, QW = BC / 8 / NW;
+  static_assert(QP * 8 * NW == BP && QW * 8 * NW == BC, "tile/wave mismatch");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave / WP, wp = wave % WP;
+  const int n_tc = a.Cout / BC;
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int tc = w % n_tc;
+  const int gp = gridDim.x / n_tc, wi = w / n_tc;
+  const int64_t tiles_p = (a.M + BP - 1) / BP;
+  const int64_t tp_begin = wi * tiles_p / gp, tp_end = (wi + 1) * tiles_p / gp;
+  if (tp_begin >= tp_end) return;  // whole workgroup (uniform)
+  const int c0 = tc * BC;
+
+  const int nk0 = a.KH * a.KW * a.Cin * ES / 128;
+  const int nk1 = a.in1 ? a.Cin1 * ES / 128 : 0;
+  const int nk = nk0 + nk1;
+  const int64_t total = (tp_end - tp_begin) * nk;
+
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.in1 ? a.in1 : a.in0), (short)0, (int)a.in1_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, (int)a.wt_bytes, 0x00020000);
+  const int ps0 = (int)a.in0_pstride * ES, ps1 = (int)a.in1_pstride * ES;
+  const int HoWo = a.Ho * a.Wo;
+  const int lrow = lane >> 3;
+
+  // weights: fixed for the workgroup (channel tile tc)
+  const int ktot_b = nk * 128;
+  int woff[QW];
+#pragma unroll
+  for (int i = 0; i < QW; ++i) {
+    const int r = 8 * (wave + NW * i) + lrow;               // weight row (channel) in the tile
+    const int c = (lane & 7) ^ (((BP + r) >> 1) & 7);       // swizzle key of LDS row BP + r
+    woff[i] = (c0 + r) * ktot_b + c * 16;
+  }
+  // bias of this lane's output channels: [i][r] = bias[c0 + wc*16*TC + i*16 + (lane>>4)*4 + r]
+  float bias[TC][4];
+#pragma unroll
+  for (int i = 0; i < TC; ++i) {
+    const float4 b4 = *(const float4*)(a.bias + c0 + wc * 16 * TC + i * 16 + (lane >> 4) * 4);
+    bias[i][0] = b4.x; bias[i][1] = b4.y; bias[i][2] = b4.z; bias[i][3] = b4.w;
+  }
+
+  // ---- issue-side state: pixel-row metadata of the tile being DMA'd
+  int poff0[QP], poff1[QP], piy[QP], pix[QP];
+  int64_t itile = tp_begin;
+  int iks = 0;
+  auto set_tile = [&](int64_t tp) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < QP; ++i) {
+      const int r = 8 * (wave + NW * i) + lrow;
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int64_t m = tp * BP + r;
+      if (m < a.M) {
+        const int b = (int)(m / HoWo);
+        const int rem = (int)(m - (int64_t)b * HoWo);
+        const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
+        piy[i] = oy * a.stride - a.pad;
+        pix[i] = ox * a.stride - a.pad;
+        poff0[i] = ((b * a.H + piy[i]) * a.W + pix[i]) * ps0 + c * 16;
+        poff1[i] = ((b * a.H1 + oy * a.ss1) * a.W1 + ox * a.ss1) * ps1 + c * 16;
+      } else {
+        piy[i] = -0x4000;
+        pix[i] = -0x4000;
+        poff0[i] = 0;
+        poff1[i] = 0x7FFF0000;  // + K offset (< 64 KB) stays past num_records
+      }
+    }
+  };
+  set_tile(itile);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  auto issue = [&](int st) __attribute__((always_inline)) {
+    const unsigned sb = lds0 + st * STAGE;
+    if (iks < nk0) {
+      const int kpt = a.Cin * ES / 128;  // K-steps per tap
+      const int tap = iks / kpt;
+      const int ci = iks - tap * kpt;
+      const int ky = tap / a.KW, kx = tap - ky * a.KW;
+      const int toff = (ky * a.W + kx) * ps0 + ci * 128;
+#pragma unroll
+      for (int i = 0; i < QP; ++i) {
+        const int iy = piy[i] + ky, ix = pix[i] + kx;
+        const bool ok = ((unsigned)iy < (unsigned)a.H) && ((unsigned)ix < (unsigned)a.W);
+        dma16(r0, ok ? poff0[i] + toff : 0x7FFFFFF0, sb + (wave + NW * i) * 1024);
+      }
+    } else {
+      const int toff = (iks - nk0) * 128;
+#pragma unroll
+      for (int i = 0; i < QP; ++i) dma16(r1, poff1[i] + toff, sb + (wave + NW * i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < QW; ++i) dma16(rw, woff[i] + iks * 128, sb + BP * 128 + (wave + NW * i) * 1024);
+    if (++iks == nk) {
+      iks = 0;
+      if (++itile < tp_end) set_tile(itile);
+    }
+  };
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fg = lane >> 4;
+  issue(0);
+  if (S == 3 && total > 1) issue(1);
+  int st = 0, cks = 0;
+  int64_t ctile = tp_begin;
+  T* __restrict__ out = (T*)a.out;
+  for (int64_t g = 0; g < total; ++g) {
+    // retire this wave's DMA for step g (S = 3: step g+1's stays in flight;
+    // epilogue stores issued since are waited for conservatively), then the
+    // barrier publishes every wave's step-g data and frees the stage the next
+    // issue overwrites.
+    if (S == 3 && g + 1 < total)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QP + QW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (g + S - 1 < total) issue(S == 3 ? (st == 0 ? 2 : st - 1) : (st ^ 1));
+    const char* base = smem + st * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      uint4 wf[TC], pf[TP];
+      const int c = fg + 4 * s;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const int r = BP + wc * 16 * TC + i * 16 + fr;
+        wf[i] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int r = wp * 16 * TP + j * 16 + fr;
+        pf[j] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pf[j], acc[i][j]);
+    }
+    st = st + 1 == S ? 0 : st + 1;
+    if (++cks == nk) {
+      // ---- register epilogue: lane holds channels co..co+3 of pixel px
+      cks = 0;
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int64_t px = ctile * BP + wp * 16 * TP + j * 16 + fr;
+        if (px < a.M) {
+#pragma unroll
+          for (int i = 0; i < TC; ++i) {
+            const int co = c0 + wc * 16 * TC + i * 16 + fg * 4;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[r] = acc[i][j][r] + bias[i][r];
+              if (a.relu) v[r] = fmaxf(v[r], 0.f);
+            }
+            T* op = out + px * a.out_pstride + co;
+            if constexpr (sizeof(T) == 2) {
+              uint2 q;
+              q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+              q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+              *(uint2*)op = q;
+            } else {
+              *(float4*)op = make_float4(v[0], v[1], v[2], v[3]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ++ctile;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <typename T, int WC, int WP, int TC, int TP, int S, int OCC>
+static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
+  constexpr int smem = block_smem_bytes<WC, WP, TC, TP, S>();
+  static_assert(smem * OCC <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  constexpr int BC = 16 * TC * WC, BP = 16 * TP * WP;
+  const int occupancy = OCC;
+  SAD_REQUIRE(a.Cout % BC == 0, "Cout must be a multiple of the channel tile");
+  const int n_tc = a.Cout / BC;
+  const int64_t tiles_p = (a.M + BP - 1) / BP;
+  int64_t g = std::min<int64_t>(tiles_p * n_tc, (int64_t)256 * occupancy);
+  g = std::max<int64_t>(n_tc, g / n_tc * n_tc);
+  hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC>), dim3((unsigned)g), dim3(64 * WC * WP), smem, s, a);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
+}
+
+// Variants (channels x pixels tile, waves, wave tile, ring stages, LDS, workgroups/CU):
+//  9: 64x256  4w 64x64  S2  80 KB 2     10: 128x128 4w 64x64  S2  64 KB 2
+// 11: 64x256  4w 64x64  S3 120 KB 1     12: 128x128 4w 64x64  S3  96 KB 1
+// 13: 256x256 8w 128x64 S2 128 KB 1     14: 128x256 8w 64x64  S2  96 KB 1
+// 15: 128x256 8w 64x64  S3 144 KB 1     16: 64x512  8w 64x64  S2 144 KB 1
+// 17: 256x128 4w 128x64 S2  96 KB 1     18: 128x256 4w 64x128 S2  96 KB 1
+template <typename T>
+static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
+  switch (v) {
+    case 9: return launch_block_t<T, 1, 4, 4, 4, 2, 2>(a, s);
+    case 10: return launch_block_t<T, 2, 2, 4, 4, 2, 2>(a, s);
+    case 11: return launch_block_t<T, 1, 4, 4, 4, 3, 1>(a, s);
+    case 12: return launch_block_t<T, 2, 2, 4, 4, 3, 1>(a, s);
+    case 13: return launch_block_t<T, 2, 4, 8, 4, 2, 1>(a, s);
+    case 14: return launch_block_t<T, 2, 4, 4, 4, 2, 1>(a, s);
+    case 15: return launch_block_t<T, 2, 4, 4, 4, 3, 1>(a, s);
+    case 16: return launch_block_t<T, 1, 8, 4, 4, 2, 1>(a, s);
+    case 17: return launch_block_t<T, 2, 2, 8, 4, 2, 1>(a, s);
+    case 18: return launch_block_t<T, 2, 2, 4, 8, 2, 1>(a, s);
+  }
+  set_error("unknown block-conv variant");
+  return SAD_ERR_ARG;
+}
+
+int default_block_variant(const BlockConvArgs& a) { return a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? 10 : 9); }
+static bool variant_fits(int v, int cout) {
+  const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128};
+  return v >= 9 && v <= 18 && cout % bc[v] == 0;
+}
+
+int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int variant) {
+  const int ES = dtype == SAD_BF16 ? 2 : 4;
+  BlockConvArgs a = a_in;
+  a.in0_bytes = (((int64_t)a.N * a.H * a.W - 1) * a.in0_pstride + a.Cin) * ES;
+  a.in1_bytes = a.in1 ? (((int64_t)a.N * a.H1 * a.W1 - 1) * a.in1_pstride + a.Cin1) * ES : 0;
+  a.wt_bytes = (int64_t)a.Cout * (a.KH * a.KW * a.Cin + (a.in1 ? a.Cin1 : 0)) * ES;
+  SAD_REQUIRE(a.in0_bytes < (1ll << 31) - 65536 && a.in1_bytes < (1ll << 31) - 65536 && a.wt_bytes < (1ll << 31),
+              "block conv operand exceeds the 2 GiB buffer range (lower the micro-batch)");
+  SAD_REQUIRE((a.Cin * ES) % 128 == 0 && (!a.in1 || (a.Cin1 * ES) % 128 == 0),
+              "channels must fill whole 128-B K-steps");
+  SAD_REQUIRE(a.Cout % 64 == 0 && a.out_pstride % 4 == 0, "Cout / output stride");
+  SAD_REQUIRE(a.in0_pstride % (16 / ES) == 0 && (!a.in1 || a.in1_pstride % (16 / ES) == 0), "input strides");
+  if (a.M == 0) return SAD_OK;
+  const int v = variant > 0 ? variant : default_block_variant(a);
+  SAD_REQUIRE(variant_fits(v, a.Cout), "variant's channel tile does not divide Cout");
+  return dtype == SAD_BF16 ? launch_block_v<u16>(a, v, s) : launch_block_v<float>(a, v, s);
+}
+
+}  // namespace sad

@@ -21,6 +21,24 @@ struct ConvArgs {
   int64_t wt_bytes;      // set by launch_conv
 };
 
+// One GEMM = 3x3 (or 1x1) conv of source 0 + optional 1x1 shortcut of source 1
+// (identity or downsample), BN folded, K axis concatenated (block.hip).
+struct BlockConvArgs {
+  const void* in0;       // NHWC [N, H, W, *], pixel stride in0_pstride (elements)
+  int64_t in0_pstride;
+  int N, H, W, Cin, KH, KW, stride, pad;
+  const void* in1;       // optional shortcut source NHWC [N, H1, W1, *]; pixel (oy*ss1, ox*ss1)
+  int64_t in1_pstride;
+  int H1, W1, Cin1, ss1;
+  const void* wt;        // [Cout][KH*KW*Cin + Cin1] (dtype)
+  const float* bias;     // [Cout]
+  void* out;             // [M, *] pixel stride out_pstride
+  int64_t out_pstride;
+  int Ho, Wo, Cout, relu;
+  int64_t M;
+  int64_t in0_bytes, in1_bytes, wt_bytes;  // set by launch_block_conv
+};
+
 struct StemArgs {
   const float* map;      // [B, mh, mw] standardised maps (bilinearly resized in-kernel), or
   const float* img;      // [B, 512, 512] fp32 image (one channel of the reference's 3 identical
@@ -37,6 +55,7 @@ struct StemArgs {
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s, int variant = 0);
 int default_conv_variant(const ConvArgs& a);
 int launch_stem(const StemArgs& a, int dtype, hipStream_t s);
+int launch_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, int variant = 0);
 int launch_avgpool(const void* in, int64_t B, int hw, int c, float* out, int dtype, hipStream_t s);
 int launch_heads_final(const float* y2, int64_t B, int n_heads, const float* w3, const float* b3,
                        float* logits, float* merged, hipStream_t s);

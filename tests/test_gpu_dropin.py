@@ -116,3 +116,43 @@ def test_conv_op_fp32_vs_torch(N, H, Cin, Cout, k, s, p, res):
         ref = ref.clamp_min(0).float()
         err = (y - ref).abs().max().item() / ref.abs().max().item()
         assert err <= 1e-5, (v, err)
+
+
+@pytest.mark.parametrize('N,H,Cin,Cout,stride,shortcut', [
+    (3, 20, 64, 64, 1, 'identity'),     # layer1-style block conv2 + identity, ragged M
+    (2, 18, 64, 128, 2, None),          # block conv1 with stride 2
+    (2, 16, 128, 128, 1, 'ds'),         # conv2 + downsample shortcut from a 32x32 input
+    (1, 8, 512, 512, 1, 'identity'),    # deep K
+])
+def test_block_conv_fp32_vs_torch(N, H, Cin, Cout, stride, shortcut):
+    """conv + shortcut as one GEMM == torch conv2d + (identity | 1x1/2 conv) + bias, ReLU."""
+    from sad.engine import block_conv
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, Cin, device=DEV)
+    w = torch.randn(Cout, 3, 3, Cin, device=DEV) * (2.0 / (9 * Cin)) ** 0.5
+    b = torch.randn(Cout, device=DEV)
+    Ho = (H + 2 - 3) // stride + 1
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(0, 3, 1, 2).double(), b.double(), stride, 1)
+    if shortcut == 'identity':
+        sc = torch.randn(N, Ho, Ho, Cout, device=DEV)
+        wsc = torch.eye(Cout, device=DEV)
+        ref = ref + sc.permute(0, 3, 1, 2).double()
+        ss = 1
+    elif shortcut == 'ds':
+        Cs = 64
+        sc = torch.randn(N, 2 * Ho, 2 * Ho, Cs, device=DEV)
+        wsc = torch.randn(Cout, Cs, device=DEV) * 0.1
+        ref = ref + F.conv2d(sc.permute(0, 3, 1, 2).double(), wsc.double()[:, :, None, None], None, 2)
+        ss = 2
+    else:
+        sc, wsc, ss = None, None, 1
+    wcat = w.reshape(Cout, -1) if sc is None else torch.cat([w.reshape(Cout, -1), wsc], 1)
+    ref = ref.permute(0, 2, 3, 1).clamp_min(0).float()
+    bc = {9: 64, 10: 128, 11: 64, 12: 128, 13: 256, 14: 128, 15: 128, 16: 64, 17: 256, 18: 128}
+    for v in [0] + [v for v in bc if Cout % bc[v] == 0]:
+        y = block_conv(x, wcat.contiguous(), b, stride, 1, sc, ss, True, v)
+        err = (y - ref).abs().max().item() / ref.abs().max().item()
+        assert err <= 1e-5, (v, err)
+    yb = block_conv(x.bfloat16(), wcat.contiguous().bfloat16(), b, stride, 1,
+                    None if sc is None else sc.bfloat16(), ss, True)
+    assert (yb.float() - ref).abs().max().item() / ref.abs().max().item() <= 3e-2

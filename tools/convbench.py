@@ -38,7 +38,11 @@ def main():
     ap.add_argument('--variants', type=int, nargs='+', default=[1, 2, 3, 4, 5, 6, 7, 8])
     ap.add_argument('--iters', type=int, default=10)
     ap.add_argument('--shapes', nargs='*', default=None)
+    ap.add_argument('--blocks', action='store_true', help='sweep the block-conv kernel (variants 9-12)')
     args = ap.parse_args()
+    if args.blocks:
+        bench_blocks(args.mb, [v for v in args.variants if v >= 9] or list(range(9, 19)), args.iters, args.shapes)
+        return
     dev = torch.device('cuda:0')
     torch.manual_seed(0)
     for name, H, Cin, Cout, k, s, p, res in SHAPES:
@@ -78,6 +82,64 @@ def main():
                 ts.sort()
                 t = ts[len(ts) // 2]
                 print(f'{name:8s} mb={mb:4d} v={v}: {t * 1e3:9.1f} us  {flop / t / 1e9:7.1f} TF/s  {same}', flush=True)
+
+
+BLOCKS = [  # name, H(in), Cin, Cout, stride, shortcut
+    ('l1.c2+id', 128, 64, 64, 1, 'id'),
+    ('l2.c1', 128, 64, 128, 2, None),
+    ('l2.c2+ds', 64, 128, 128, 1, 'ds'),
+    ('l2.c2+id', 64, 128, 128, 1, 'id'),
+    ('l3.c1', 64, 128, 256, 2, None),
+    ('l3.c2+ds', 32, 256, 256, 1, 'ds'),
+    ('l3.c2+id', 32, 256, 256, 1, 'id'),
+    ('l4.c1', 32, 256, 512, 2, None),
+    ('l4.c2+ds', 16, 512, 512, 1, 'ds'),
+    ('l4.c2+id', 16, 512, 512, 1, 'id'),
+]
+
+
+def bench_blocks(mbs, variants, iters, shapes=None):
+    from sad.engine import block_conv
+    dev = torch.device('cuda:0')
+    for name, H, Cin, Cout, s, sc in BLOCKS:
+        if shapes and name not in shapes:
+            continue
+        Ho = H // s
+        cin0 = Cin if sc is None else Cout
+        h0 = H if sc is None else Ho
+        K = 9 * cin0 + (0 if sc is None else (Cout if sc == 'id' else Cin))
+        w = (torch.randn(Cout, K, device=dev) * (1.0 / K) ** 0.5).to(torch.bfloat16)
+        bias = torch.randn(Cout, device=dev) * 0.1
+        for mb in mbs:
+            x = torch.randn(mb, h0, h0, cin0, device=dev).to(torch.bfloat16)
+            scx = None
+            if sc == 'id':
+                scx = torch.randn(mb, Ho, Ho, Cout, device=dev).to(torch.bfloat16)
+            elif sc == 'ds':
+                scx = torch.randn(mb, 2 * Ho, 2 * Ho, Cin, device=dev).to(torch.bfloat16)
+            stride = s if sc is None else 1
+            flop = 2.0 * mb * Ho * Ho * Cout * K
+            ref = None
+            bc = {9: 64, 10: 128, 11: 64, 12: 128, 13: 256, 14: 128, 15: 128, 16: 64, 17: 256, 18: 128}
+            for v in variants:
+                if Cout % bc[v]:
+                    continue
+                out = block_conv(x, w, bias, stride, 1, scx, 2 if sc == 'ds' else 1, True, v)
+                torch.cuda.synchronize()
+                same = 'ref' if ref is None else ('same' if torch.equal(out, ref) else
+                                                  f'DIFF {(out.float() - ref.float()).abs().max().item():.3g}')
+                ref = out.clone() if ref is None else ref
+                ts = []
+                for _ in range(iters):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    block_conv(x, w, bias, stride, 1, scx, 2 if sc == 'ds' else 1, True, v, out)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+                ts.sort()
+                t = ts[len(ts) // 2]
+                print(f'{name:9s} mb={mb:4d} v={v}: {t * 1e3:9.1f} us  {flop / t / 1e9:7.1f} TF/s  {same}', flush=True)
 
 
 if __name__ == '__main__':
