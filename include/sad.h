@@ -167,17 +167,21 @@ int sad_conv2d_run(const void* in, int64_t N, int32_t H, int32_t W, int32_t Cin,
                    int32_t stride, int32_t pad, int32_t relu, int32_t dtype, int32_t variant,
                    void* stream);
 
-/* One GEMM = conv(in0) + 1x1 shortcut(in1) (+ bias, optional ReLU) on the
- * persistent block-conv kernel the backbone uses for timm's BasicBlock
- * (conv2 -> bn2 -> + shortcut -> act2, the shortcut being the identity or
- * downsample.0/1).  wt: [Cout][k*k*Cin + Cin1] -- the shortcut's weights
- * (identity matrix or folded 1x1 conv) are the last Cin1 K columns; in1 may be
- * NULL (plain conv).  Shortcut pixel = (oy*ss1, ox*ss1) of in1 [N,H1,W1,Cin1].
- * variant: 0 = default, 9..12 = tile variants (csrc/block.hip). */
+/* One GEMM = conv(in0) + 1x1 shortcut(in1) (+ bias [+ res], optional ReLU) on
+ * the block-conv kernels the backbone uses for timm's BasicBlock (conv2 -> bn2
+ * -> + shortcut -> act2, the shortcut being the identity or downsample.0/1).
+ * wt: [Cout][wt_ld] with wt_ld >= k*k*Cin + Cin1 (0 = exactly that): the conv
+ * taps, then the shortcut's weights (identity matrix or folded 1x1 conv) as the
+ * next Cin1 K columns; in1 may be NULL (plain conv).  Shortcut pixel =
+ * (oy*ss1, ox*ss1) of in1 [N,H1,W1,Cin1].  res (NULL or NHWC [N,Ho,Wo,Cout],
+ * same dtype) is an identity shortcut added in the epilogue instead; it needs
+ * the halo kernel (bf16, 3x3/s1/p1, H and W multiples of 16).
+ * variant: 0 = default, 9..18 = implicit-GEMM tiles, 20 = halo (block.hip, halo.hip). */
 int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* in1,
-                       int32_t H1, int32_t W1, int32_t Cin1, int32_t ss1, const void* wt,
-                       const float* bias, void* out, int32_t Cout, int32_t k, int32_t stride,
-                       int32_t pad, int32_t relu, int32_t dtype, int32_t variant, void* stream);
+                       int32_t H1, int32_t W1, int32_t Cin1, int32_t ss1, const void* wt, int32_t wt_ld,
+                       const float* bias, const void* res, void* out, int32_t Cout, int32_t k,
+                       int32_t stride, int32_t pad, int32_t relu, int32_t dtype, int32_t variant,
+                       void* stream);
 
 /* -------------------------------------------------------------- synthetic */
 /* Deterministic synthetic segments; bit-identical to

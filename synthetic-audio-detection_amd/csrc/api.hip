@@ -296,11 +296,18 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
       b2.H = b2.W = Ho;
       b2.Cin = blk.cout;
       b2.stride = 1;
-      b2.in1 = bufA;
-      b2.in1_pstride = C;
-      b2.H1 = b2.W1 = H;
-      b2.Cin1 = C;
-      b2.ss1 = blk.stride;
+      b2.wt_ld = 9 * blk.cout + blk.cin_sc;
+      if (p->dtype == SAD_BF16 && blk.stride == 1 && blk.cout == 64 && Ho % 16 == 0) {
+        // layer1 identity blocks: the shortcut is an epilogue add on the halo kernel
+        b2.res = bufA;
+        b2.res_pstride = C;
+      } else {
+        b2.in1 = bufA;
+        b2.in1_pstride = C;
+        b2.H1 = b2.W1 = H;
+        b2.Cin1 = C;
+        b2.ss1 = blk.stride;
+      }
       b2.wt = blk.w2;
       b2.bias = blk.b2;
       b2.out = bufB;
@@ -615,8 +622,9 @@ extern "C" int sad_conv2d_run(const void* in, int64_t N, int32_t H, int32_t W, i
 
 extern "C" int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* in1,
                                   int32_t H1, int32_t W1, int32_t Cin1, int32_t ss1, const void* wt,
-                                  const float* bias, void* out, int32_t Cout, int32_t k, int32_t stride,
-                                  int32_t pad, int32_t relu, int32_t dtype, int32_t variant, void* stream) {
+                                  int32_t wt_ld, const float* bias, const void* res, void* out, int32_t Cout,
+                                  int32_t k, int32_t stride, int32_t pad, int32_t relu, int32_t dtype,
+                                  int32_t variant, void* stream) {
   SAD_REQUIRE(in0 && wt && bias && out, "null tensor");
   SAD_REQUIRE(N >= 0 && H > 0 && W > 0 && k > 0 && stride > 0 && pad >= 0, "bad shape");
   SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
@@ -637,7 +645,10 @@ extern "C" int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t
   a.Cin1 = in1 ? Cin1 : 0;
   a.ss1 = ss1;
   a.wt = wt;
+  a.wt_ld = wt_ld;
   a.bias = bias;
+  a.res = res;
+  a.res_pstride = Cout;
   a.out = out;
   a.out_pstride = Cout;
   a.Ho = (H + 2 * pad - k) / stride + 1;
@@ -646,5 +657,6 @@ extern "C" int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t
   a.Cout = Cout;
   a.relu = relu;
   a.M = N * a.Ho * a.Wo;
-  return launch_block_conv(a, dtype, (hipStream_t)stream, variant);
+  a.ablate = variant >> 8;  // timing-only ablation bits (tools/convbench.py --ablate)
+  return launch_block_conv(a, dtype, (hipStream_t)stream, variant & 255);
 }

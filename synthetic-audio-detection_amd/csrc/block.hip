@@ -78,7 +78,7 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   const int lrow = lane >> 3;
 
   // weights: fixed for the workgroup (channel tile tc)
-  const int ktot_b = nk * 128;
+  const int ktot_b = a.wt_ld * ES;
   int woff[QW];
 #pragma unroll
   for (int i = 0; i < QW; ++i) {
@@ -166,13 +166,15 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
     // epilogue stores issued since are waited for conservatively), then the
     // barrier publishes every wave's step-g data and frees the stage the next
     // issue overwrites.
-    if (S == 3 && g + 1 < total)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QP + QW) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!(a.ablate & 2)) {
+      if (S == 3 && g + 1 < total)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QP + QW) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (!(a.ablate & 4)) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (g + S - 1 < total) issue(S == 3 ? (st == 0 ? 2 : st - 1) : (st ^ 1));
+    if (g + S - 1 < total && !(a.ablate & 1)) issue(S == 3 ? (st == 0 ? 2 : st - 1) : (st ^ 1));
     const char* base = smem + st * STAGE;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -278,9 +280,21 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
   return SAD_ERR_ARG;
 }
 
-int default_block_variant(const BlockConvArgs& a) { return a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? 10 : 9); }
+int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s);
+
+// halo kernel (variant 20): bf16 stride-1 3x3 with Cout = 64 (layer1), where the
+// implicit GEMM is L2->LDS-fill bound; it is also the only one taking `res`.
+static bool halo_ok(const BlockConvArgs& a, int dtype) {
+  return dtype == SAD_BF16 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.in1 && a.Cin % 64 == 0 &&
+         a.Cout % 64 == 0 && a.W % 16 == 0 && a.H % 16 == 0;
+}
+int default_block_variant(const BlockConvArgs& a, int dtype) {
+  if (halo_ok(a, dtype) && (a.Cout == 64 || a.res)) return 20;
+  return a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? 10 : 9);
+}
 static bool variant_fits(int v, int cout) {
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128};
+  if (v == 20) return cout % 64 == 0;
   return v >= 9 && v <= 18 && cout % bc[v] == 0;
 }
 
@@ -289,16 +303,25 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   BlockConvArgs a = a_in;
   a.in0_bytes = (((int64_t)a.N * a.H * a.W - 1) * a.in0_pstride + a.Cin) * ES;
   a.in1_bytes = a.in1 ? (((int64_t)a.N * a.H1 * a.W1 - 1) * a.in1_pstride + a.Cin1) * ES : 0;
-  a.wt_bytes = (int64_t)a.Cout * (a.KH * a.KW * a.Cin + (a.in1 ? a.Cin1 : 0)) * ES;
-  SAD_REQUIRE(a.in0_bytes < (1ll << 31) - 65536 && a.in1_bytes < (1ll << 31) - 65536 && a.wt_bytes < (1ll << 31),
+  if (a.wt_ld == 0) a.wt_ld = a.KH * a.KW * a.Cin + (a.in1 ? a.Cin1 : 0);
+  SAD_REQUIRE(a.wt_ld >= a.KH * a.KW * a.Cin + (a.in1 ? a.Cin1 : 0) && (a.wt_ld * ES) % 16 == 0, "weight row length");
+  a.wt_bytes = (int64_t)a.Cout * a.wt_ld * ES;
+  a.res_bytes = a.res ? (a.M - 1) * a.res_pstride * ES + a.Cout * ES : 0;
+  SAD_REQUIRE(a.in0_bytes < (1ll << 31) - 65536 && a.in1_bytes < (1ll << 31) - 65536 && a.wt_bytes < (1ll << 31) &&
+                  a.res_bytes < (1ll << 31) - 65536,
               "block conv operand exceeds the 2 GiB buffer range (lower the micro-batch)");
   SAD_REQUIRE((a.Cin * ES) % 128 == 0 && (!a.in1 || (a.Cin1 * ES) % 128 == 0),
               "channels must fill whole 128-B K-steps");
   SAD_REQUIRE(a.Cout % 64 == 0 && a.out_pstride % 4 == 0, "Cout / output stride");
   SAD_REQUIRE(a.in0_pstride % (16 / ES) == 0 && (!a.in1 || a.in1_pstride % (16 / ES) == 0), "input strides");
   if (a.M == 0) return SAD_OK;
-  const int v = variant > 0 ? variant : default_block_variant(a);
+  const int v = variant > 0 ? variant : default_block_variant(a, dtype);
   SAD_REQUIRE(variant_fits(v, a.Cout), "variant's channel tile does not divide Cout");
+  if (v == 20) {
+    SAD_REQUIRE(halo_ok(a, dtype), "halo conv (variant 20): bf16, 3x3/s1/p1, no GEMM shortcut, H, W % 16");
+    return launch_halo_v(a, v, s);
+  }
+  SAD_REQUIRE(!a.res, "an epilogue residual needs the halo kernel (variant 20)");
   return dtype == SAD_BF16 ? launch_block_v<u16>(a, v, s) : launch_block_v<float>(a, v, s);
 }
 

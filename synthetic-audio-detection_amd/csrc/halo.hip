@@ -1,0 +1,401 @@
+// halo.hip -- persistent halo-tile direct conv for layer1's stride-1 3x3 convs
+// (bf16, gfx950).
+//
+// Contract: BlockConvArgs with KH = KW = 3, stride 1, pad 1, no in1; the
+// optional identity shortcut comes in as `res` and is added in the epilogue:
+//   out = act(conv3x3(in0) + bias [+ res])
+// These are timm BasicBlock conv1 / conv2(+identity) of layer1
+// (inference_runner.py:49-51 -> timm resnet18).
+//
+// Why a second kernel: block.hip's implicit GEMM DMAs every input pixel row
+// once per filter tap, and for Cout = 64 that stream (≈52 FLOP per DMA byte)
+// caps it at the CU's L2->LDS fill rate (≈70 GB/s/CU, MI355X_MICROARCH
+// "gather into LDS"), i.e. ~1/3 of MFMA peak.  Here a workgroup owns a TH x TW
+// output tile and DMAs the (TH+2) x (TW+2) input patch of each 64-channel
+// chunk ONCE, serving all 9 taps from it; the identity shortcut costs an
+// epilogue add instead of a 10th K-step.
+//
+// Pipeline -- one barrier per K-step, two wave roles (one of each per SIMD):
+//  * weight waves (0 .. NW/2-1): DMA the BC x 64 weight slice of step g+4 into
+//    a 5-stage ring during step g (counted vmcnt): an LDS-DMA takes ~1 us from
+//    issue to landing even from L2, longer than a step, so one step of lead
+//    time made the step time the DMA latency;
+//  * patch waves (NW/2 .. NW-1): during taps 0-3 of chunk u, DMA the patch of
+//    chunk u+1 (double buffer) and, in a tile's last chunk, during taps 2-5 the
+//    tile's residual rows; they wait only before the first step of the next
+//    chunk -- first-touch (HBM / MALL) data gets >= 4 steps of cover;
+//  * the epilogue of tile t runs right after the barrier of tile t+1's first
+//    step (its residual rows are published by that barrier): every wave adds
+//    bias [+ residual], applies the activation and writes bf16 in place over
+//    the residual rows; after the next barrier the patch waves store the tile
+//    as full 128-B pixel rows (1 KB per wave-instruction).  Only patch waves
+//    store, so the weight waves' counted waits see DMAs only.
+//  * operands swapped (C = W . X^T): each lane holds 4 consecutive output
+//    channels of one pixel.
+#include <utility>
+
+#include "common.hpp"
+#include "igemm.hpp"
+#include "kernels.hpp"
+
+namespace sad {
+
+// f(std::integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// LDS chunk swizzle of the halo kernel: chunk c of row r sits at c ^ (r & 6).
+// Conflict-free for ds_read_b128 fragment reads of 16 consecutive rows at ANY
+// row offset (the kx taps shift a fragment by one row); igemm.hpp's swz is
+// conflict-free only for even offsets (exhaustive check over the b128 lane
+// groups of MI355X_MICROARCH.md "LDS").
+__device__ __forceinline__ int hswz(int row, int chunk) { return chunk ^ (row & 6); }
+
+template <int WC, int WP, int TC, int TP, int TW>
+struct HaloGeo {
+  static constexpr int NW = WC * WP;
+  static constexpr int NL = NW / 2;             // waves per role
+  static constexpr int BC = 16 * TC * WC;       // channels per tile
+  static constexpr int BP = 16 * TP * WP;       // pixels per tile
+  static constexpr int TH = BP / TW;
+  static constexpr int PW = TW + 2, PH = TH + 2;
+  static constexpr int PR = PW * PH;            // patch rows (pixels)
+  static constexpr int NDP = (PR + 7) / 8;      // DMA wave-instructions per patch
+  static constexpr int QP = (NDP + NL - 1) / NL;  // per patch wave
+  static constexpr int NDR = BP / 8;            // residual DMAs per tile
+  static constexpr int QR = NDR / NL;
+  static constexpr int QW = BC / 8 / NL;        // weight DMAs per weight wave per step
+  static constexpr int PATCH = NDP * 1024;
+  static constexpr int RES = BP * 128;
+  static constexpr int WST = BC * 128;
+  static constexpr int NWS = 5;                 // weight ring stages (NWS-1 steps ahead)
+  static constexpr int OFF_RES = 2 * PATCH, OFF_W = 2 * PATCH + RES;
+  static constexpr int SMEM = OFF_W + NWS * WST;
+  static_assert(TW == 16, "a 16-pixel fragment is one tile row");
+  static_assert(BP % TW == 0 && NW % 2 == 0, "tile shape");
+  static_assert(NDR % NL == 0 && BC % (8 * NL) == 0, "DMA split");
+  static_assert(QP <= 12, "patch pieces must fit taps 0-3 at 3 per step");
+};
+
+template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU>
+__global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(BlockConvArgs a) {
+  using G = HaloGeo<WC, WP, TC, TP, TW>;
+  constexpr int NL = G::NL, BC = G::BC, TH = G::TH, PW = G::PW, PR = G::PR;
+  constexpr int QP = G::QP, QR = G::QR, QW = G::QW, NDP = G::NDP, NWS = G::NWS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool wloader = wave < NL;  // weight wave, else patch wave
+  const int lw = wloader ? wave : wave - NL;
+  const int wc = wave / WP, wp = wave % WP;
+  const int n_tc = a.Cout / BC;
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int tc = w % n_tc;
+  const int gp = gridDim.x / n_tc, wi = w / n_tc;
+  const int tiles_x = a.W / TW, tiles_img = tiles_x * (a.H / TH);
+  const int tiles_p = a.N * tiles_img;
+  const int tp_begin = (int)((int64_t)wi * tiles_p / gp), tp_end = (int)((int64_t)(wi + 1) * tiles_p / gp);
+  if (tp_begin >= tp_end) return;
+  const int c0 = tc * BC;
+  const int nc0 = a.Cin / 64;  // 64-channel chunks, 9 taps each
+
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, (int)a.wt_bytes, 0x00020000);
+  const int ps0 = (int)a.in0_pstride * 2;
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+  // ---- weight waves: their rows of the (fixed) channel tile; K cursor of the next DMA
+  int woff[QW];
+#pragma unroll
+  for (int i = 0; i < QW; ++i) {
+    const int r = 8 * (lw + NL * i) + (lane >> 3);
+    woff[i] = (c0 + r) * (a.wt_ld * 2) + ((lane & 7) ^ (r & 6)) * 16;
+  }
+  int wtap = 0, wch = 0, wsi = 0;
+  auto load_weights = [&]() __attribute__((always_inline)) {
+    const int kb = (wtap * nc0 + wch) * 128;
+#pragma unroll
+    for (int i = 0; i < QW; ++i) dma16_m0(rw, woff[i] + kb, lds0 + G::OFF_W + wsi * G::WST + (lw + NL * i) * 1024);
+    if (++wtap == 9) {
+      wtap = 0;
+      if (++wch == nc0) wch = 0;
+    }
+    wsi = wsi + 1 == NWS ? 0 : wsi + 1;
+  };
+
+  // ---- patch waves: per piece k, the source offset of the (tile, chunk) being loaded
+  int poff[QP];
+  int ltile = tp_begin, lch = 0;
+  auto prep_patch = [&]() __attribute__((always_inline)) {
+    const bool live = ltile < tp_end;  // past the WG's last tile: all-zero pieces
+    const int b = ltile / tiles_img, rem = ltile - b * tiles_img;
+    const int oy0 = (rem / tiles_x) * TH, ox0 = (rem % tiles_x) * TW;
+#pragma unroll
+    for (int k = 0; k < QP; ++k) {
+      const int pr = 8 * (lw + NL * k) + (lane >> 3);
+      const int py = pr / PW, px = pr - py * PW;
+      const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+      poff[k] = (live && pr < PR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+                    ? ((b * a.H + iy) * a.W + ix) * ps0 + lch * 128 + ((lane & 7) ^ (pr & 6)) * 16
+                    : 0x7FFFFFF0;  // padding / past the patch: zeros
+    }
+  };
+  auto advance_patch = [&]() __attribute__((always_inline)) {
+    if (++lch == nc0) {
+      lch = 0;
+      ++ltile;
+    }
+    prep_patch();
+  };
+  auto res_pieces = [&](int t, int tap) __attribute__((always_inline)) {
+    if constexpr (RES) {
+      const __amdgpu_buffer_rsrc_t rr =
+          __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.res_bytes, 0x00020000);
+      const int b = t / tiles_img, rem = t - b * tiles_img;
+      const int oy0 = (rem / tiles_x) * TH, ox0 = (rem % tiles_x) * TW;
+#pragma unroll
+      for (int k = 0; k < QR; ++k) {
+        if (k % 4 != tap - 2) continue;
+        const int q = lw + NL * k;
+        const int p = 8 * q + (lane >> 3);
+        const int ty = p / TW, tx = p - ty * TW;
+        const int off = ((b * a.H + oy0 + ty) * a.W + ox0 + tx) * (int)a.res_pstride * 2 +
+                        (c0 / 8 + ((lane & 7) ^ (p & 6))) * 16;
+        dma16_m0(rr, off, lds0 + G::OFF_RES + q * 1024);
+      }
+    }
+  };
+
+  float bias[TC][4];
+#pragma unroll
+  for (int i = 0; i < TC; ++i) {
+    const float4 b4 = *(const float4*)(a.bias + c0 + wc * 16 * TC + i * 16 + (lane >> 4) * 4);
+    bias[i][0] = b4.x;
+    bias[i][1] = b4.y;
+    bias[i][2] = b4.z;
+    bias[i][3] = b4.w;
+  }
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fg = lane >> 4;
+  // fragment j of this wave = tile row ty = wp*TP + j, pixels fr = 0..15
+  // epilogue, part 1 (every wave, tap 0 of the next tile): bias [+ residual],
+  // activation, bf16 -> the tile's LDS staging rows (in place over the
+  // residual rows: each lane writes exactly the bytes it read)
+  auto epilogue = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      const int p = (wp * TP + j) * TW + fr;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const int cl = wc * 16 * TC + i * 16 + fg * 4;
+        uint2* sp = (uint2*)(smem + G::OFF_RES + p * 128 + (hswz(p, cl >> 3) << 4) + (cl & 7) * 2);
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[i][r];
+        if constexpr (RES) {
+          const uint2 rv = *sp;
+          v[0] += __uint_as_float(rv.x << 16);
+          v[1] += __uint_as_float(rv.x & 0xFFFF0000u);
+          v[2] += __uint_as_float(rv.y << 16);
+          v[3] += __uint_as_float(rv.y & 0xFFFF0000u);
+        }
+        if constexpr (RELU)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        uint2 qv;
+        qv.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        qv.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *sp = qv;
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  // epilogue, part 2 (patch waves, tap 1, after a barrier): staging rows ->
+  // global, 8 pixels x 128 B per wave-instruction (full lines)
+  auto store_tile = [&](int t) __attribute__((always_inline)) {
+    const int b = t / tiles_img, rem = t - b * tiles_img;
+    const int oy0 = (rem / tiles_x) * TH, ox0 = (rem % tiles_x) * TW;
+    u16* __restrict__ out = (u16*)a.out + ((int64_t)(b * a.Ho + oy0) * a.Wo + ox0) * a.out_pstride + c0;
+#pragma unroll
+    for (int k = 0; k < QR; ++k) {
+      const int p = 8 * (lw + NL * k) + (lane >> 3), c = lane & 7;
+      const uint4 v = *(const uint4*)(smem + G::OFF_RES + p * 128 + (hswz(p, c) << 4));
+      const int ty = p / TW, tx = p - ty * TW;
+      *(uint4*)(out + (ty * a.Wo + tx) * (int)a.out_pstride + c * 8) = v;
+    }
+  };
+
+  // ---- one K-step from LDS: two K-halves (s = 0, 1); half 1's reads are
+  // issued between half 0's MFMAs
+  auto compute_step = [&](int tap, int wst, int pbuf) __attribute__((always_inline)) {
+    const char* pb = smem + pbuf * G::PATCH;
+    const char* wb = smem + G::OFF_W + wst * G::WST;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    uint4 w[2][TC], p[2][TP];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = fg + 4 * s;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const int r = wc * 16 * TC + i * 16 + fr;
+        w[s][i] = *(const uint4*)(wb + r * 128 + (hswz(r, c) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int r = (wp * TP + j + ky) * PW + kx + fr;
+        p[s][j] = *(const uint4*)(pb + r * 128 + (hswz(r, c) << 4));
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) mfma_chunk<u16>(w[s][i], p[s][j], acc[i][j]);
+    // schedule: half 0's reads, then its MFMAs interleaved with half 1's reads
+    __builtin_amdgcn_sched_group_barrier(0x100, TC + TP, 0);
+#pragma unroll
+    for (int k = 0; k < TC + TP; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * TC * TP - (TC + TP), 0);
+  };
+
+  // ---- prologue: patch of the first chunk, weights of the first NWS-1 steps,
+  // fragments of step 0
+  if (wloader) {
+#pragma unroll
+    for (int k = 0; k < NWS - 1; ++k) load_weights();
+  } else {
+    prep_patch();
+#pragma unroll
+    for (int k = 0; k < QP; ++k)
+      if (NDP % NL == 0 || lw + NL * k < NDP) dma16_m0(r0, poff[k], lds0 + (lw + NL * k) * 1024);
+    advance_patch();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // One chunk = 9 K-steps (taps) of tile t, channel chunk ch, unrolled so every
+  // tap-dependent decision is static.  Each step: wait -> barrier -> DMA issue
+  // -> [epilogue of the previous tile] -> step g from LDS.  Past the last step the weight waves keep issuing
+  // (wrapped K cursor) and the patch waves issue all-zero pieces, so the
+  // counted waits never change shape; nothing reads those stages.
+  int t = tp_begin, ch = 0, wsc = 0, pbuf = 0;
+  const int ab = a.ablate;
+  auto chunk = [&]() __attribute__((always_inline)) {
+    const bool after_tile = t > tp_begin && ch == 0;   // tile t-1's epilogue stores go out at tap 0
+    const bool last_chunk = ch + 1 == nc0;
+    static_for<9>([&](auto tap_c) __attribute__((always_inline)) {
+      constexpr int tap = decltype(tap_c)::value;
+      if (!(ab & 2)) {
+        if (wloader) {
+          // w(g) was issued at step g-4; younger: w(g+1..g+3) (weight waves store nothing)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * QW) : "memory");
+        } else if (tap == 0) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next chunk's patch + this tile's residual
+        }
+      }
+      if constexpr (tap == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging rows written
+      if (!(ab & 4)) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(ab & 1)) {
+        if (wloader) {
+          load_weights();
+        } else {
+          if constexpr (tap < 4) {
+#pragma unroll
+            for (int k = tap; k < QP; k += 4)
+              if (NDP % NL == 0 || lw + NL * k < NDP)
+                dma16_m0(r0, poff[k], lds0 + (pbuf ^ 1) * G::PATCH + (lw + NL * k) * 1024);
+            if constexpr (tap == 3) advance_patch();
+          }
+          if constexpr (tap == 1)
+            if (after_tile) store_tile(t - 1);
+          if constexpr (RES && tap >= 2 && tap <= 5)
+            if (last_chunk) res_pieces(t, tap);
+        }
+      }
+      if constexpr (tap == 0)
+        if (after_tile && !(ab & 8)) epilogue();
+      compute_step(tap, wsc, pbuf);
+      wsc = wsc + 1 == NWS ? 0 : wsc + 1;
+    });
+    pbuf ^= 1;
+    if (++ch == nc0) {
+      ch = 0;
+      ++t;
+    }
+  };
+  const int nchunks = (tp_end - tp_begin) * nc0;
+  for (int c = 0; c < nchunks; ++c) chunk();
+  // last tile: its residual rows were issued in its last chunk; publish, then store
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  epilogue();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (!wloader) store_tile(tp_end - 1);
+}
+
+template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU>
+static int launch_halo_t(const BlockConvArgs& a, hipStream_t s) {
+  using G = HaloGeo<WC, WP, TC, TP, TW>;
+  static_assert(G::SMEM <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)halo_conv_kernel<WC, WP, TC, TP, TW, RES, RELU>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+    attr = true;
+  }
+  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.in1,
+              "halo conv: 3x3, stride 1, pad 1, no GEMM shortcut");
+  SAD_REQUIRE(a.Cin % 64 == 0 && a.Cout % G::BC == 0, "halo conv: Cin % 64, Cout % channel tile");
+  SAD_REQUIRE(a.W % TW == 0 && a.H % G::TH == 0 && a.Ho == a.H && a.Wo == a.W, "image must tile exactly");
+  SAD_REQUIRE(a.wt_ld >= 9 * a.Cin && (a.wt_ld * 2) % 16 == 0, "weight row length");
+  SAD_REQUIRE(!a.res || a.res_pstride >= a.Cout, "residual pixel stride");
+  SAD_REQUIRE(a.out_pstride * 2 * (int64_t)a.M < (1ll << 40), "output too large");
+  const int n_tc = a.Cout / G::BC;
+  const int64_t tiles_p = (int64_t)a.N * (a.H / G::TH) * (a.W / TW);
+  SAD_REQUIRE(tiles_p * 9 * (a.Cin / 64) < (1ll << 31), "too many tiles for one launch");
+  int64_t g = std::min<int64_t>(tiles_p * n_tc, 256);
+  g = std::max<int64_t>(n_tc, g / n_tc * n_tc);
+  hipLaunchKernelGGL((halo_conv_kernel<WC, WP, TC, TP, TW, RES, RELU>), dim3((unsigned)g), dim3(64 * WC * WP),
+                     G::SMEM, s, a);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
+}
+
+template <int WC, int WP, int TC, int TP, int TW>
+static int launch_halo_g(const BlockConvArgs& a, hipStream_t s) {
+  if (a.res) return a.relu ? launch_halo_t<WC, WP, TC, TP, TW, true, true>(a, s)
+                           : launch_halo_t<WC, WP, TC, TP, TW, true, false>(a, s);
+  return a.relu ? launch_halo_t<WC, WP, TC, TP, TW, false, true>(a, s)
+                : launch_halo_t<WC, WP, TC, TP, TW, false, false>(a, s);
+}
+
+// Variants (channels x tile (TH x TW), waves, wave tile, LDS; one WG per CU):
+//  20: 64 x 16x16  8w  64x32  154 KB
+int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s) {
+  switch (v) {
+    case 20: return launch_halo_g<1, 8, 4, 2, 16>(a, s);
+  }
+  set_error("unknown halo-conv variant");
+  return SAD_ERR_ARG;
+}
+
+}  // namespace sad

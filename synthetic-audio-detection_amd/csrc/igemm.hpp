@@ -17,6 +17,22 @@ struct DT<float> {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return (chunk ^ ((row >> 1) & 7)); }
 
+// Same, M0 declared clobbered instead of saved/restored (2 fewer SALU per DMA;
+// hipcc re-materialises M0 where it needs it, which in these kernels is nowhere
+// inside the main loop).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma16_m0(__amdgpu_buffer_rsrc_t rsrc, int voff, unsigned lds_base) {
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %2, 0 offen lds"
+      :
+      : "v"(voff), "s"(__builtin_amdgcn_readfirstlane(lds_base)), "s"(rsrc)
+      : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 // One LDS-DMA wave-instruction: 16 B per lane from buffer offset `voff` to LDS
 // [lds_base + 16*lane].  M0 (compiler-reserved) is saved/restored inside the
 // statement; offsets past the buffer's num_records load zeros.

@@ -30,13 +30,18 @@ struct BlockConvArgs {
   const void* in1;       // optional shortcut source NHWC [N, H1, W1, *]; pixel (oy*ss1, ox*ss1)
   int64_t in1_pstride;
   int H1, W1, Cin1, ss1;
-  const void* wt;        // [Cout][KH*KW*Cin + Cin1] (dtype)
+  const void* wt;        // [Cout][wt_ld] (dtype): KH*KW*Cin conv taps, then Cin1 shortcut columns
+  int wt_ld;             // elements per weight row; 0 = KH*KW*Cin + Cin1
   const float* bias;     // [Cout]
+  const void* res;       // optional residual added before the activation, NHWC [M, *] (halo kernel only)
+  int64_t res_pstride;
   void* out;             // [M, *] pixel stride out_pstride
   int64_t out_pstride;
   int Ho, Wo, Cout, relu;
   int64_t M;
-  int64_t in0_bytes, in1_bytes, wt_bytes;  // set by launch_block_conv
+  int64_t in0_bytes, in1_bytes, wt_bytes, res_bytes;  // set by launch_block_conv
+  int ablate;            // timing ablations (wrong results): 1 no DMA in loop, 2 no vmcnt wait, 4 no barrier,
+                         // 8 no epilogue (halo)
 };
 
 struct StemArgs {

@@ -57,8 +57,8 @@ SIGNATURES = {
     'sad_heads_workspace_size': (ctypes.c_int, [P, I64, ctypes.POINTER(SZ)]),
     'sad_heads_merge_run': (ctypes.c_int, [P, FPP, I64, P, P, P, SZ, P]),
     'sad_conv2d_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P]),
-    'sad_block_conv_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, I32, I32, I32, I32, P, P, P, I32, I32, I32,
-                                          I32, I32, I32, I32, P]),
+    'sad_block_conv_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, I32, I32, I32, I32, P, I32, P, P, P, I32, I32,
+                                          I32, I32, I32, I32, I32, P]),
     'sad_synth_pcm': (ctypes.c_int, [ctypes.c_uint64, I64, I64, I32, P, P]),
 }
 

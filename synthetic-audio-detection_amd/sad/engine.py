@@ -299,14 +299,14 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int = 1
 
 def block_conv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int = 1, pad: int = 1,
                sc: torch.Tensor | None = None, sc_stride: int = 1, relu: bool = True, variant: int = 0,
-               out: torch.Tensor | None = None) -> torch.Tensor:
-    """conv(x) + 1x1 shortcut(sc) as ONE GEMM (libsad block-conv kernel).
-    x [N,H,W,Cin], sc [N,H1,W1,Cin1] or None, w [Cout, k*k*Cin + Cin1] (the
-    shortcut's weights are the last Cin1 columns), bias [Cout] fp32."""
+               out: torch.Tensor | None = None, res: torch.Tensor | None = None, k: int = 3) -> torch.Tensor:
+    """conv(x) + 1x1 shortcut(sc) [+ res] as ONE launch (libsad block-conv kernels).
+    x [N,H,W,Cin], sc [N,H1,W1,Cin1] or None, w [Cout, wt_ld] with the k*k*Cin
+    conv taps first and the shortcut's Cin1 columns next (extra columns are
+    ignored), bias [Cout] fp32, res [N,Ho,Wo,Cout] (epilogue identity shortcut)."""
     N, H, W, Cin = x.shape
     Cout = w.shape[0]
     Cin1 = sc.shape[3] if sc is not None else 0
-    k = int(round(((w.shape[1] - Cin1) / Cin) ** 0.5))
     Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
     dt = _lib.SAD_BF16 if x.dtype == torch.bfloat16 else _lib.SAD_F32
     if out is None:
@@ -314,6 +314,6 @@ def block_conv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int
     H1, W1 = (sc.shape[1], sc.shape[2]) if sc is not None else (0, 0)
     with torch.cuda.device(x.device):
         _lib.call('sad_block_conv_run', _lib.ptr(x), N, H, W, Cin, _lib.ptr(sc), H1, W1, Cin1, sc_stride,
-                  _lib.ptr(w), _lib.ptr(bias), _lib.ptr(out), Cout, k, stride, pad, int(relu), dt, variant,
-                  _lib.stream_handle(x.device))
+                  _lib.ptr(w), w.stride(0), _lib.ptr(bias), _lib.ptr(res), _lib.ptr(out), Cout, k, stride, pad,
+                  int(relu), dt, variant, _lib.stream_handle(x.device))
     return out

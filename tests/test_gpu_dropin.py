@@ -123,6 +123,12 @@ def test_conv_op_fp32_vs_torch(N, H, Cin, Cout, k, s, p, res):
     (2, 18, 64, 128, 2, None),          # block conv1 with stride 2
     (2, 16, 128, 128, 1, 'ds'),         # conv2 + downsample shortcut from a 32x32 input
     (1, 8, 512, 512, 1, 'identity'),    # deep K
+    (2, 16, 64, 64, 1, 'identity'),     # halo (16x16 tiles), layer1-style, one tile per image
+    (3, 48, 64, 64, 1, None),           # halo, plain conv1, 9 tiles per image, fewer tiles than CUs
+    (16, 128, 64, 64, 1, 'identity'),   # halo at layer1's map size, several tiles per workgroup
+    (2, 32, 128, 64, 1, 'identity'),    # halo, two 64-channel chunks per tile
+    (2, 32, 128, 128, 1, 'ds'),         # downsample shortcut from 64x64
+    (1, 16, 512, 512, 1, 'identity'),   # deep K, Cout 512
 ])
 def test_block_conv_fp32_vs_torch(N, H, Cin, Cout, stride, shortcut):
     """conv + shortcut as one GEMM == torch conv2d + (identity | 1x1/2 conv) + bias, ReLU."""
@@ -149,10 +155,21 @@ def test_block_conv_fp32_vs_torch(N, H, Cin, Cout, stride, shortcut):
     wcat = w.reshape(Cout, -1) if sc is None else torch.cat([w.reshape(Cout, -1), wsc], 1)
     ref = ref.permute(0, 2, 3, 1).clamp_min(0).float()
     bc = {9: 64, 10: 128, 11: 64, 12: 128, 13: 256, 14: 128, 15: 128, 16: 64, 17: 256, 18: 128}
-    for v in [0] + [v for v in bc if Cout % bc[v] == 0]:
+    vs = [0] + [v for v in bc if Cout % bc[v] == 0]
+    for v in vs:
         y = block_conv(x, wcat.contiguous(), b, stride, 1, sc, ss, True, v)
         err = (y - ref).abs().max().item() / ref.abs().max().item()
         assert err <= 1e-5, (v, err)
-    yb = block_conv(x.bfloat16(), wcat.contiguous().bfloat16(), b, stride, 1,
-                    None if sc is None else sc.bfloat16(), ss, True)
+    # bf16: default kernel choice (the halo kernel for Cout 64 without a GEMM shortcut)
+    wb = wcat.contiguous().bfloat16()
+    yb = block_conv(x.bfloat16(), wb, b, stride, 1, None if sc is None else sc.bfloat16(), ss, True)
     assert (yb.float() - ref).abs().max().item() / ref.abs().max().item() <= 3e-2
+    if stride == 1 and H % 16 == 0 and shortcut != 'ds':
+        # halo kernel, identity shortcut as an epilogue residual; the weight rows keep
+        # their (unused) identity columns, as the backbone plan stores them
+        res = None if sc is None else sc.bfloat16()
+        yh = block_conv(x.bfloat16(), wb, b, 1, 1, None, 1, True, 20, res=res)
+        assert (yh.float() - ref).abs().max().item() / ref.abs().max().item() <= 3e-2
+        # same bf16 operands through the implicit-GEMM kernel: the two agree to bf16 rounding
+        yg = block_conv(x.bfloat16(), wb, b, 1, 1, res, 1, True, 9)
+        assert (yh.float() - yg.float()).abs().max().item() / yg.float().abs().max().item() <= 1e-2

@@ -38,10 +38,12 @@ def main():
     ap.add_argument('--variants', type=int, nargs='+', default=[1, 2, 3, 4, 5, 6, 7, 8])
     ap.add_argument('--iters', type=int, default=10)
     ap.add_argument('--shapes', nargs='*', default=None)
-    ap.add_argument('--blocks', action='store_true', help='sweep the block-conv kernel (variants 9-12)')
+    ap.add_argument('--blocks', action='store_true', help='sweep the block-conv kernels (variants 9-18, 20)')
+    ap.add_argument('--ablate', type=int, nargs='+', default=[0], help='block kernel timing ablations (bit mask)')
     args = ap.parse_args()
     if args.blocks:
-        bench_blocks(args.mb, [v for v in args.variants if v >= 9] or list(range(9, 19)), args.iters, args.shapes)
+        bench_blocks(args.mb, [v for v in args.variants if v >= 9] or list(range(9, 19)) + [20], args.iters, args.shapes,
+                     tuple(args.ablate))
         return
     dev = torch.device('cuda:0')
     torch.manual_seed(0)
@@ -98,7 +100,7 @@ BLOCKS = [  # name, H(in), Cin, Cout, stride, shortcut
 ]
 
 
-def bench_blocks(mbs, variants, iters, shapes=None):
+def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,)):
     from sad.engine import block_conv
     dev = torch.device('cuda:0')
     for name, H, Cin, Cout, s, sc in BLOCKS:
@@ -120,11 +122,17 @@ def bench_blocks(mbs, variants, iters, shapes=None):
             stride = s if sc is None else 1
             flop = 2.0 * mb * Ho * Ho * Cout * K
             ref = None
-            bc = {9: 64, 10: 128, 11: 64, 12: 128, 13: 256, 14: 128, 15: 128, 16: 64, 17: 256, 18: 128}
-            for v in variants:
-                if Cout % bc[v]:
+            bc = {9: 64, 10: 128, 11: 64, 12: 128, 13: 256, 14: 128, 15: 128, 16: 64, 17: 256, 18: 128, 20: 64}
+            for v0 in [v + (ab << 8) for v in variants for ab in ablate]:
+                v = v0 & 255
+                if Cout % bc[v] or (v == 20 and (stride != 1 or sc == 'ds')):
                     continue
-                out = block_conv(x, w, bias, stride, 1, scx, 2 if sc == 'ds' else 1, True, v)
+                # the halo kernel (20) takes the identity shortcut as an epilogue residual
+                kw = dict(res=scx) if v == 20 else dict(sc=scx, sc_stride=2 if sc == 'ds' else 1)
+
+                def run(o=None):
+                    return block_conv(x, w, bias, stride, 1, relu=True, variant=v0, out=o, **kw)
+                out = run()
                 torch.cuda.synchronize()
                 same = 'ref' if ref is None else ('same' if torch.equal(out, ref) else
                                                   f'DIFF {(out.float() - ref.float()).abs().max().item():.3g}')
@@ -133,13 +141,14 @@ def bench_blocks(mbs, variants, iters, shapes=None):
                 for _ in range(iters):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    block_conv(x, w, bias, stride, 1, scx, 2 if sc == 'ds' else 1, True, v, out)
+                    run(out)
                     e1.record()
                     torch.cuda.synchronize()
                     ts.append(e0.elapsed_time(e1))
                 ts.sort()
                 t = ts[len(ts) // 2]
-                print(f'{name:9s} mb={mb:4d} v={v}: {t * 1e3:9.1f} us  {flop / t / 1e9:7.1f} TF/s  {same}', flush=True)
+                print(f'{name:9s} mb={mb:4d} v={v} ablate={v0 >> 8}: {t * 1e3:9.1f} us  {flop / t / 1e9:7.1f} TF/s  {same}',
+                      flush=True)
 
 
 if __name__ == '__main__':
