@@ -297,8 +297,8 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
       b2.Cin = blk.cout;
       b2.stride = 1;
       b2.wt_ld = 9 * blk.cout + blk.cin_sc;
-      if (p->dtype == SAD_BF16 && blk.stride == 1 && blk.cout == 64 && Ho % 16 == 0) {
-        // layer1 identity blocks: the shortcut is an epilogue add on the halo kernel
+      if (p->dtype == SAD_BF16 && blk.stride == 1 && blk.cout <= 128 && Ho % 16 == 0) {
+        // identity blocks of layer1/2: the shortcut is an epilogue add on the halo kernel
         b2.res = bufA;
         b2.res_pstride = C;
       } else {

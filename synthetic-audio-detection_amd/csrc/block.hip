@@ -282,14 +282,17 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
 
 int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s);
 
-// halo kernel (variant 20): bf16 stride-1 3x3 with Cout = 64 (layer1), where the
-// implicit GEMM is L2->LDS-fill bound; it is also the only one taking `res`.
+// halo kernel (variant 20): bf16 stride-1 3x3 with Cout <= 128 (layer1, layer2's
+// second block), where the implicit GEMM is L2->LDS-fill bound (convbench,
+// mb 128: layer1 c2 261 vs 350 us, layer2 c1 187 vs 218 us); for Cout >= 256
+// the patch would be re-loaded per 64-channel tile.  It is also the only
+// kernel taking `res`.
 static bool halo_ok(const BlockConvArgs& a, int dtype) {
   return dtype == SAD_BF16 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.in1 && a.Cin % 64 == 0 &&
          a.Cout % 64 == 0 && a.W % 16 == 0 && a.H % 16 == 0;
 }
 int default_block_variant(const BlockConvArgs& a, int dtype) {
-  if (halo_ok(a, dtype) && (a.Cout == 64 || a.res)) return 20;
+  if (halo_ok(a, dtype) && (a.Cout <= 128 || a.res)) return 20;
   return a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? 10 : 9);
 }
 static bool variant_fits(int v, int cout) {

@@ -315,8 +315,8 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
       __builtin_amdgcn_sched_barrier(0);
       if (!(ab & 1)) {
         if (wloader) {
-          load_weights();
-        } else {
+          if (!(ab & 16)) load_weights();
+        } else if (!(ab & 32)) {
           if constexpr (tap < 4) {
 #pragma unroll
             for (int k = tap; k < QP; k += 4)

@@ -91,6 +91,7 @@ BLOCKS = [  # name, H(in), Cin, Cout, stride, shortcut
     ('l2.c1', 128, 64, 128, 2, None),
     ('l2.c2+ds', 64, 128, 128, 1, 'ds'),
     ('l2.c2+id', 64, 128, 128, 1, 'id'),
+    ('l2.c1b', 64, 128, 128, 1, None),
     ('l3.c1', 64, 128, 256, 2, None),
     ('l3.c2+ds', 32, 256, 256, 1, 'ds'),
     ('l3.c2+id', 32, 256, 256, 1, 'id'),
