@@ -428,58 +428,137 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
 }
 
 // ------------------------------------------------------------ stem, bf16 --
-// Throughput-mode stem.  K is laid out (ky, kx) on an 8 x 8 grid (ky = 7 and
-// kx = 7 carry zero weights), so the 8 consecutive k of one MFMA lane fragment
-// are 8 consecutive image pixels of ONE row: 4 x ds_read_b32 from a bf16 image
-// band (row pitch 272 dwords = 16 banks mod 32, conflict-free for the 4 lane
-// groups).  A workgroup produces STEM_P pooled rows: conv rows 2*py0-1 ..
-// 2*(py0+P)-1 (2P+1 rows for P pooled rows), vertical max carried in registers.
+// Throughput-mode stem: conv1 7x7/2 (BN folded, 3 identical input channels
+// folded into one) -> ReLU -> maxpool 3x3/2, one launch (inference_runner.py:
+// 49-51 via timm resnet18 conv1/bn1/act1/maxpool).
+//
+// K is laid out (ky, kx) on an 8 x 8 grid (ky = 7 and kx = 7 carry zero
+// weights), so the 8 consecutive k of one MFMA fragment are 8 consecutive
+// image pixels of ONE row: 4 x ds_read_b32 from a bf16 image band (row pitch
+// 272 dwords = 16 banks mod 32: conflict-free).  Operands are swapped
+// (C = W . img^T): a lane holds 4 consecutive channels of one conv pixel.
+//
+// A workgroup produces STEM_P pooled rows (conv rows 2*py0-1 .. 2*(py0+P)-1).
+// Max-pool runs on the raw accumulators -- bias and ReLU are monotonic, so
+// relu(max(x) + b) == max(relu(x + b)) and rounding once to bf16 after the
+// pool equals rounding before it: vertical max in registers, horizontal max by
+// DPP row shifts (lane fr <- fr +- 1 within a 16-pixel block, block edges by
+// row_shl:15, wave edges through LDS).  The resize is separable: map rows are
+// x-interpolated once per workgroup into LDS, then each band pixel is one
+// y-lerp (same arithmetic as bilinear512).
 constexpr int STEM_P = 4;
-constexpr int STEM_BAND_ROWS = 4 * STEM_P + 8;
-constexpr int STEM_BPITCH = 544;  // bf16 elements per band row (>= 518)
+constexpr int STEM_BAND_ROWS = 4 * STEM_P + 8;  // 4P+7 with non-zero weights
+constexpr int STEM_BPITCH = 544;                 // bf16 elements per band row (>= 518)
+constexpr int STEM_HROWS = 10;                   // x-interpolated map rows kept in LDS
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
 
 __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
   __shared__ __attribute__((aligned(16))) u16 s_img[STEM_BAND_ROWS * STEM_BPITCH];
   __shared__ __attribute__((aligned(16))) u16 s_w[64 * 72];
-  __shared__ __attribute__((aligned(16))) u16 s_pool[256 * 64];
+  __shared__ __attribute__((aligned(16))) float s_bias[64];
+  // x-interpolated map rows while the band is built; afterwards the pooled-row
+  // staging [128 q][64 ch] bf16 and the wave-edge exchange [4][64] fp32
+  __shared__ __attribute__((aligned(16))) float s_u[STEM_HROWS * 512];
+  u16* s_out = (u16*)s_u;
+  float* s_edge = s_u + 128 * 64 / 2;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int py0 = blockIdx.x * STEM_P;
   const int64_t b = blockIdx.y;
-  const float* __restrict__ map = a.img ? nullptr : a.map + b * a.mh * a.mw;
   for (int i = tid; i < 64 * 8; i += 256) {  // [64 co][64 k] bf16 -> pitch 72
     const int co = i >> 3, c8 = (i & 7) * 8;
     *(uint4*)(s_w + co * 72 + c8) = *(const uint4*)((const u16*)a.w + co * 64 + c8);
   }
-  // image band: rows iy = 4*py0 - 5 + tr, cols ix = tc - 3 (zero outside 512x512)
-  const float sh = (float)a.mh / 512.f, sw = (float)a.mw / 512.f;
-  for (int i = tid; i < STEM_BAND_ROWS * STEM_BPITCH; i += 256) {
-    const int tr = i / STEM_BPITCH, tc = i - tr * STEM_BPITCH;
-    const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
-    float v = 0.f;
-    if ((unsigned)iy < 512u && (unsigned)ix < 512u)
-      v = a.img ? a.img[(b * 512 + iy) * 512 + ix] : bilinear512(map, a.mh, a.mw, sh, sw, iy, ix);
-    s_img[i] = f2bf(v);
+  if (tid < 64) s_bias[tid] = a.bias[tid];
+  // ---- image band: rows iy = 4*py0 - 5 + tr, cols ix = tc - 3 (zero outside 512x512)
+  // every band row a fragment reads, incl. the zero-weight tap row ky = 7
+  // (uninitialised LDS could hold NaN, and NaN * 0 is NaN)
+  constexpr int NBR = STEM_BAND_ROWS;
+  if (a.img) {
+    for (int i = tid; i < NBR * STEM_BPITCH; i += 256) {
+      const int tr = i / STEM_BPITCH, tc = i - tr * STEM_BPITCH;
+      const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
+      float v = 0.f;
+      if ((unsigned)iy < 512u && (unsigned)ix < 512u) v = a.img[(b * 512 + iy) * 512 + ix];
+      s_img[i] = f2bf(v);
+    }
+  } else {
+    const float* __restrict__ map = a.map + b * a.mh * a.mw;
+    const float sh = (float)a.mh / 512.f, sw = (float)a.mw / 512.f;
+    auto src_row = [&](int iy, int& y0, int& y1, float& ly) {
+      float fy = sh * (iy + 0.5f) - 0.5f;
+      fy = fy < 0.f ? 0.f : fy;
+      y0 = min((int)floorf(fy), a.mh - 1);
+      y1 = min(y0 + 1, a.mh - 1);
+      ly = fminf(fmaxf(fy - y0, 0.f), 1.f);
+    };
+    const int iy_lo = max(4 * py0 - 5, 0), iy_hi = min(4 * py0 - 5 + NBR - 1, 511);
+    int ylo, yhi, t0, t1;
+    float tl;
+    src_row(iy_lo, ylo, t0, tl);
+    src_row(iy_hi, t1, yhi, tl);
+    const int nh = yhi - ylo + 1;
+    if (nh <= STEM_HROWS) {
+      // x-lerp of map rows ylo..yhi for every image column
+      for (int i = tid; i < nh * 512; i += 256) {
+        const int r = i >> 9, ix = i & 511;
+        float fx = sw * (ix + 0.5f) - 0.5f;
+        fx = fx < 0.f ? 0.f : fx;
+        const int x0 = min((int)floorf(fx), a.mw - 1), x1 = min(x0 + 1, a.mw - 1);
+        const float lx = fminf(fmaxf(fx - x0, 0.f), 1.f);
+        const float* mr = map + (ylo + r) * a.mw;
+        s_u[i] = (1.f - lx) * mr[x0] + lx * mr[x1];
+      }
+      __syncthreads();
+      for (int i = tid; i < NBR * STEM_BPITCH; i += 256) {
+        const int tr = i / STEM_BPITCH, tc = i - tr * STEM_BPITCH;
+        const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
+        float v = 0.f;
+        if ((unsigned)iy < 512u && (unsigned)ix < 512u) {
+          int y0, y1;
+          float ly;
+          src_row(iy, y0, y1, ly);
+          v = (1.f - ly) * s_u[(y0 - ylo) * 512 + ix] + ly * s_u[(y1 - ylo) * 512 + ix];
+        }
+        s_img[i] = f2bf(v);
+      }
+    } else {  // very tall maps: direct bilinear per pixel
+      for (int i = tid; i < NBR * STEM_BPITCH; i += 256) {
+        const int tr = i / STEM_BPITCH, tc = i - tr * STEM_BPITCH;
+        const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
+        float v = 0.f;
+        if ((unsigned)iy < 512u && (unsigned)ix < 512u) v = bilinear512(map, a.mh, a.mw, sh, sw, iy, ix);
+        s_img[i] = f2bf(v);
+      }
+    }
   }
-  __syncthreads();
-  const int fr = lane & 15, fg = lane >> 4;
-  uint4 bw[4][2];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) bw[j][s] = *(const uint4*)(s_w + (j * 16 + fr) * 72 + 32 * s + 8 * fg);
-  float bias[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) bias[j] = a.bias[j * 16 + fr];
+  __syncthreads();  // band complete; s_u is free from here on
 
-  // conv row cr (relative band row of its first tap = 2*(cr - 2*py0) + 2)
+  const int fr = lane & 15, fg = lane >> 4;
+
+  // raw conv row cr for this wave's 64 conv columns: r[i][j] = C[ch j*16+fg*4+e][px 64w+16i+fr]
   auto conv_row = [&](int cr, f32x4 (&r)[4][4]) __attribute__((always_inline)) {
+    if (cr < 0) {  // above the image: never wins the max
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[i][j] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) r[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (cr < 0 || cr >= 256) return;  // block-uniform; zero row never wins the max
     const int rb = 2 * (cr - 2 * py0) + 2;
+    uint4 bw[4][2];  // weight fragments (LDS-resident; re-read per row keeps VGPRs for the pool)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) bw[j][s] = *(const uint4*)(s_w + (j * 16 + fr) * 72 + 32 * s + 8 * fg);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int cx = wave * 64 + i * 16 + fr;
@@ -492,21 +571,16 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
         av.z = *(const uint32_t*)(p + 4);
         av.w = *(const uint32_t*)(p + 6);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mfma_chunk<u16>(av, bw[j][s], r[i][j]);
+        for (int j = 0; j < 4; ++j) mfma_chunk<u16>(bw[j][s], av, r[i][j]);
       }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) r[i][j][e] = bf2f(f2bf(fmaxf(r[i][j][e] + bias[j], 0.f)));
   };
 
   f32x4 carry[4][4], cur[4][4];
   conv_row(2 * py0 - 1, carry);
   for (int pi = 0; pi < STEM_P; ++pi) {
     const int py = py0 + pi;
+    // vertical max over conv rows 2py-1, 2py, 2py+1 (carry holds 2py-1)
     conv_row(2 * py, cur);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -520,29 +594,51 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          s_pool[(wave * 64 + i * 16 + fg * 4 + e) * 64 + j * 16 + fr] = f2bf(fmaxf(cur[i][j][e], carry[i][j][e]));
+        for (int e = 0; e < 4; ++e) cur[i][j][e] = fmaxf(cur[i][j][e], carry[i][j][e]);
+    // wave edge: conv column 64w-1 comes from wave w-1 (its block 3, lane fr = 15)
+    if (fr == 15) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *(float4*)(s_edge + wave * 64 + j * 16 + fg * 4) = make_float4(cur[3][j][0], cur[3][j][1], cur[3][j][2], cur[3][j][3]);
+    }
+    __syncthreads();
+    // horizontal max (pooled q = 32w + 8i + fr/2 from even lanes: cols 2q-1, 2q, 2q+1),
+    // then bias, ReLU, bf16 -> staging
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 bj = *(const float4*)(s_bias + j * 16 + fg * 4);
+        const float bias[4] = {bj.x, bj.y, bj.z, bj.w};
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = cur[i][j][e];
+          const float right = dppf<0x101>(x);  // row_shl:1  (fr + 1)
+          const float left_in = dppf<0x111>(x);  // row_shr:1  (fr - 1)
+          float left_blk;
+          if (i > 0)
+            left_blk = dppf<0x10F>(cur[i - 1][j][e]);  // row_shl:15 (lane 0 <- 15 of block i-1)
+          else
+            left_blk = wave > 0 ? s_edge[(wave - 1) * 64 + j * 16 + fg * 4 + e] : -INFINITY;
+          const float left = fr == 0 ? left_blk : left_in;
+          o[e] = fmaxf(fmaxf(fmaxf(x, right), left) + bias[e], 0.f);
+        }
+        if ((fr & 1) == 0) {
+          const int q = wave * 32 + i * 8 + (fr >> 1);
+          uint2 qv;
+          qv.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+          qv.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+          *(uint2*)(s_out + q * 64 + j * 16 + fg * 4) = qv;
+        }
+      }
+    }
     __syncthreads();
     u16* __restrict__ out = (u16*)a.out + ((b * 128 + py) * 128) * 64;
-    for (int it = tid; it < 128 * 8; it += 256) {
-      const int q = it >> 3, c0 = (it & 7) * 8;
-      float m[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) m[e] = 0.f;
-#pragma unroll
-      for (int d = -1; d <= 1; ++d) {
-        const int px = 2 * q + d;
-        if (px < 0) continue;  // px <= 255 always
-        const uint4 v = *(const uint4*)(s_pool + px * 64 + c0);
-        const u16* h = (const u16*)&v;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], bf2f(h[e]));
-      }
-      uint4 qv;
-      u16* h = (u16*)&qv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) h[e] = f2bf(m[e]);
-      *(uint4*)(out + q * 64 + c0) = qv;
+    for (int k = 0; k < 4; ++k) {
+      const int idx = (k * 256 + tid) * 8;  // 16 KB row, 16 B per thread per k
+      *(uint4*)(out + idx) = *(const uint4*)(s_out + idx);
     }
     __syncthreads();
   }
