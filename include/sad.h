@@ -183,6 +183,93 @@ int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t W, int32_t
                        int32_t stride, int32_t pad, int32_t relu, int32_t dtype, int32_t variant,
                        void* stream);
 
+/* --------------------------------------------------------------- training */
+/* The submodel_trainer.py hot path: the train-mode
+ * front end of SpectrogramDataset.__getitem__ (:139-214, transforms :463-471),
+ * and the train-mode ResNet-18 forward (BatchNorm with batch statistics) plus
+ * the backward / clip / AdamW of train() (:250-302, setup :606-660).  These are
+ * op-level entries; sad/train.py composes them into the step.  Activations are
+ * NHWC in `dtype`; statistics, gradients and master weights are fp32. */
+
+/* FrequencyMasking(15) + TimeMasking(35) (fill 0.0) on the top-db clamped dB
+ * map, then (x - mean) / (std_unbiased + 1e-6)  (:107-114,191-199).
+ * masks: device int32 [n,4] = {f0, f1, t0, t1} (rows [f0,f1), columns [t0,t1)
+ * zeroed; f0 == f1 = no mask) or NULL.  db, out_map: [n, n_mels, n_frames]. */
+int sad_specaug_norm_run(const float* db, int64_t n, int32_t n_mels, int32_t n_frames, const int32_t* masks,
+                         float* out_map, void* stream);
+/* transforms.Resize((512,512)) (:200) then RandomResizedCrop's
+ * resized_crop(i, j, h, w, (out_hw, out_hw)) (:466), one plane of the three
+ * identical channels (:203).  boxes: device int32 [n,4] = {i, j, h, w} in the
+ * 512x512 image, or NULL (= the val transform Resize((512,512)), :470). */
+int sad_crop_resize_run(const float* map, int64_t n, int32_t h, int32_t w, const int32_t* boxes, int32_t out_hw,
+                        int32_t dtype, void* img, void* stream);
+/* fp32 OIHW conv weight -> compute layout in dtype.  mode 0: [Cout][k][k][Cin]
+ * (forward); 1: [Cin][k][k][Cout] with flipped taps (stride-1 dgrad as a conv of
+ * dy); 2: [Cout][64], k = ky*7+kx, input channels summed (stem); 3: OIHW copy. */
+int sad_pack_conv_weight_run(const float* w, int32_t cout, int32_t cin, int32_t k, int32_t mode, int32_t dtype,
+                             void* out, void* stream);
+/* timm conv1 7x7/2/p3 WITHOUT bn1 (train-mode BN needs the raw output):
+ * img [n, ih, iw] (dtype) -> out NHWC [n, oh, ow, 64]; col_ws >= n*oh*ow*64
+ * elements of dtype; w_packed from mode 2. */
+int sad_stem_conv_run(const void* img, int64_t n, int32_t ih, int32_t iw, const void* w_packed, void* col_ws,
+                      size_t ws_bytes, void* out, int32_t dtype, void* stream);
+/* Workspace (bytes) of the BN entries for a [P, C] tensor. */
+int sad_bn_workspace_size(int64_t P, int32_t C, size_t* bytes);
+/* BatchNorm2d train-mode statistics of x NHWC [P, C]: stats = [mean | invstd |
+ * scale = gamma*invstd | shift = beta - mean*scale] (4*C floats); running
+ * stats (optional, both or neither) updated with momentum and the unbiased var. */
+int sad_bn_stats_run(const void* x, int64_t P, int32_t C, int32_t dtype, const float* gamma, const float* beta,
+                     float eps, float momentum, float* running_mean, float* running_var, float* stats, float* ws,
+                     size_t ws_bytes, void* stream);
+/* out = act(x*scale + shift [+ res] ) where res is added as-is (identity
+ * shortcut) or, with res_stats, as res*rscale + rshift (downsample BN). */
+int sad_bn_apply_run(const void* x, int64_t P, int32_t C, int32_t dtype, const float* stats, const void* res,
+                     const float* res_stats, int32_t relu, void* out, void* stream);
+/* bn1 + ReLU + maxpool 3x3/2/p1: x NHWC [n, H, W, C] raw conv1 -> out [n, Ho, Wo, C]. */
+int sad_bn_relu_maxpool_run(const void* x, int64_t n, int32_t H, int32_t W, int32_t C, int32_t dtype,
+                            const float* stats, void* out, void* stream);
+/* CrossEntropyLoss on logits [B, C] fp32 (the trainer's pooled features, quirk
+ * C1): dlogits = (softmax - onehot(target)) * scale; out[0] = sum of row
+ * losses, out[1] = count of rows with argmax == target; pred (optional) [B] =
+ * argmax (first maximum, outputs.max(1) at :281,346). */
+int sad_ce_loss_run(const float* logits, const int64_t* target, int64_t B, int32_t C, float scale, float* dlogits,
+                    float* out, int32_t* pred, void* stream);
+/* BatchNorm2d train-mode backward through an optional ReLU:
+ * dz = (dy | dpool[n][c]/pool_hw broadcast) * [y > 0 if y];  dbeta = sum dz,
+ * dgamma = sum dz*xhat (written, or added if accumulate);  dx = gamma*invstd*
+ * (dz - mean dz - xhat * mean(dz*xhat)).  x is the raw (pre-BN) tensor, stats
+ * from sad_bn_stats_run; dz_out (optional) receives dz. */
+int sad_bn_backward_run(const void* x, int64_t P, int32_t C, int32_t dtype, const float* stats, const float* gamma,
+                        const void* dy, const float* dpool, int32_t pool_hw, const void* y, float* dgamma,
+                        float* dbeta, int32_t accumulate, void* dz_out, void* dx, float* ws, size_t ws_bytes,
+                        void* stream);
+/* Conv weight gradient: dw [Cout][Cin][k][k] fp32 = beta*dw + sum_p dy (x) im2col(x)
+ * (im2col into col_ws: N*Ho*Wo*Cin*k*k elements of dtype; not used for 1x1/s1). */
+int sad_conv_wgrad_run(const void* x, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* dy, int32_t Cout,
+                       int32_t k, int32_t stride, int32_t pad, int32_t dtype, float beta, float* dw, void* col_ws,
+                       size_t ws_bytes, void* stream);
+/* Conv input gradient for any stride: dcol = dy * W (w_oihw from pack mode 3),
+ * col2im gather into dx NHWC [N, H, W, Cin] (added to dx if accumulate);
+ * col_ws: N*Ho*Wo*Cin*k*k fp32.  (Stride-1 3x3 dgrad runs as sad_conv2d_run
+ * over dy with pack mode 1 weights instead.) */
+int sad_conv_dgrad_run(const void* dy, int64_t N, int32_t Ho, int32_t Wo, int32_t Cout, const void* w_oihw,
+                       int32_t Cin, int32_t H, int32_t W, int32_t k, int32_t stride, int32_t pad, int32_t dtype,
+                       int32_t accumulate, void* dx, float* col_ws, size_t ws_bytes, void* stream);
+/* torch.nn.utils.clip_grad_norm_(params, max_norm) over one flat fp32 gradient
+ * buffer (:276): norm_coef[0] = ||g||, norm_coef[1] = min(max_norm/(||g||+1e-6), 1);
+ * g *= norm_coef[1].  ws >= 1024 doubles. */
+int sad_clip_grad_norm_run(float* g, int64_t n, float max_norm, float* norm_coef, void* ws, size_t ws_bytes,
+                           void* stream);
+/* torch.optim.AdamW step `step` (1-based) over flat fp32 buffers (:648-652,278). */
+int sad_adamw_run(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                  float eps, float weight_decay, int64_t step, void* stream);
+/* y += alpha * x (fp32): folds a step's layer3 gradient into its never-zeroed
+ * .grad (quirk C4: layer3 is unfrozen at epochs//3 but not in the optimizer). */
+int sad_axpy_run(float* y, const float* x, int64_t n, float alpha, void* stream);
+/* timm global average pool: x NHWC [B, hw, C] (dtype) -> out [B, C] fp32 (the
+ * trainer's model(inputs), quirk C1). */
+int sad_avgpool_run(const void* x, int64_t B, int32_t hw, int32_t C, int32_t dtype, float* out, void* stream);
+
 /* -------------------------------------------------------------- synthetic */
 /* Deterministic synthetic segments; bit-identical to
  * sad/synth.py up to rare 1-LSB float64 libm differences in the tone term.

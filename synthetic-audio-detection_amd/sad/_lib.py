@@ -60,6 +60,27 @@ SIGNATURES = {
     'sad_block_conv_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, I32, I32, I32, I32, P, I32, P, P, P, I32, I32,
                                           I32, I32, I32, I32, I32, P]),
     'sad_synth_pcm': (ctypes.c_int, [ctypes.c_uint64, I64, I64, I32, P, P]),
+    # training (include/sad.h "training")
+    'sad_specaug_norm_run': (ctypes.c_int, [P, I64, I32, I32, P, P, P]),
+    'sad_crop_resize_run': (ctypes.c_int, [P, I64, I32, I32, P, I32, I32, P, P]),
+    'sad_pack_conv_weight_run': (ctypes.c_int, [P, I32, I32, I32, I32, I32, P, P]),
+    'sad_stem_conv_run': (ctypes.c_int, [P, I64, I32, I32, P, P, SZ, P, I32, P]),
+    'sad_bn_workspace_size': (ctypes.c_int, [I64, I32, ctypes.POINTER(SZ)]),
+    'sad_bn_stats_run': (ctypes.c_int, [P, I64, I32, I32, P, P, ctypes.c_float, ctypes.c_float, P, P, P, P, SZ,
+                                        P]),
+    'sad_bn_apply_run': (ctypes.c_int, [P, I64, I32, I32, P, P, P, I32, P, P]),
+    'sad_bn_relu_maxpool_run': (ctypes.c_int, [P, I64, I32, I32, I32, I32, P, P, P]),
+    'sad_ce_loss_run': (ctypes.c_int, [P, P, I64, I32, ctypes.c_float, P, P, P, P]),
+    'sad_bn_backward_run': (ctypes.c_int, [P, I64, I32, I32, P, P, P, P, I32, P, P, P, I32, P, P, P, SZ, P]),
+    'sad_conv_wgrad_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, I32, I32, I32, I32, I32, ctypes.c_float, P, P,
+                                          SZ, P]),
+    'sad_conv_dgrad_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P,
+                                          SZ, P]),
+    'sad_clip_grad_norm_run': (ctypes.c_int, [P, I64, ctypes.c_float, P, P, SZ, P]),
+    'sad_adamw_run': (ctypes.c_int, [P, P, P, P, I64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                     ctypes.c_float, ctypes.c_float, I64, P]),
+    'sad_axpy_run': (ctypes.c_int, [P, P, I64, ctypes.c_float, P]),
+    'sad_avgpool_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, P]),
 }
 
 _lib = None

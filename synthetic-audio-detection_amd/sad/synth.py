@@ -78,6 +78,30 @@ def synth_segment(seed: int, seg: int, n: int = SEG_SAMPLES) -> np.ndarray:
     return np.clip(x, -32768, 32767).astype(np.int16)
 
 
+def synth_labelled_clip(seed: int, idx: int, label: int, n: int = 2 * SEG_SAMPLES) -> np.ndarray:
+    """Training clip with a learnable 2-class label:
+    class 1 = white noise + a harmonic tone stack (fundamental 150-600 Hz,
+    4 partials), class 0 = low-pass filtered noise (one-pole, a in [0.85, 0.97)).
+    int16 [n] (default 8 s: the trainer's two 4 s segments)."""
+    key = segment_key(seed ^ 0xC1A55, idx)
+    j = np.arange(n, dtype=np.uint64)
+    r = mix64(np.uint64(key) + (j + np.uint64(1)) * np.uint64(GOLD2))
+    u = ((r >> np.uint64(11)).astype(np.float64)) / float(1 << 53) - 0.5
+    h = mix64(key ^ 0xABCDEF)
+    if label:
+        f0 = 150.0 + (h & 0xFFFF) / 65536.0 * 450.0
+        t = np.arange(n, dtype=np.float64) / SAMPLE_RATE
+        x = 0.15 * u
+        for k in range(1, 5):
+            x += (0.2 / k) * np.sin(2.0 * np.pi * f0 * k * t + k)
+    else:
+        from scipy.signal import lfilter
+        a = 0.85 + ((h >> 16) & 0xFFFF) / 65536.0 * 0.12
+        x = lfilter([1.0 - a], [1.0, -a], u)
+        x = 0.3 * x / max(1e-9, np.abs(x).max())
+    return np.clip(np.rint(x * 32767.0), -32768, 32767).astype(np.int16)
+
+
 def synth_batch(seed: int, first_seg: int, count: int, n: int = SEG_SAMPLES) -> np.ndarray:
     """[count, n] int16, segments first_seg .. first_seg+count-1."""
     return np.stack([synth_segment(seed, first_seg + i, n) for i in range(count)]) if count else \

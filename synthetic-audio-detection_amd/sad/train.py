@@ -1,0 +1,586 @@
+"""Device training engine: the hot path of ``submodel_trainer.py`` on MI355X.
+
+What the reference does per step (``submodel_trainer.py:250-302``, model and
+optimizer from ``:606-660``), and where it runs here:
+
+* front end of ``SpectrogramDataset.__getitem__`` (``:189-208``) -- mel
+  (norm=None, quirk C3) + dB: ``FrontEnd(norm=None)``; SpecAugment masks +
+  standardise: ``sad_specaug_norm_run``; Resize(512) + RandomResizedCrop:
+  ``sad_crop_resize_run`` (``TrainFrontEnd``).
+* ``outputs = model(inputs)`` with ``model.train()``: timm ResNet-18 with
+  batch-statistics BatchNorm (running stats updated, momentum 0.1) and global
+  average pooling -> pooled features ``[B, 512]`` (the attached head is never
+  called, quirk C1): ``TrainNet.forward_train`` -- raw MFMA convs
+  (``sad_conv2d_run``, ``sad_stem_conv_run``), ``sad_bn_stats_run``,
+  ``sad_bn_apply_run`` / ``sad_bn_relu_maxpool_run``, ``sad_avgpool_run``.
+* ``CrossEntropyLoss`` on those 512 "logits": ``sad_ce_loss_run``.
+* ``loss.backward()`` into the trainable stages (layer4; layer3 once unfrozen,
+  quirk C4): ``TrainNet.backward`` -- ``sad_bn_backward_run``, dgrad as an
+  MFMA conv over flipped weights (stride 1) or GEMM + col2im (stride 2),
+  wgrad as im2col + GEMM (``sad_conv_wgrad_run``).
+* ``clip_grad_norm_(0.5)`` + ``AdamW(lr, wd=0.01)``: ``sad_clip_grad_norm_run``,
+  ``sad_adamw_run`` over flat fp32 buffers.
+* ``DataParallel`` -> one process per GPU (``torch.distributed`` over RCCL):
+  per-replica BN statistics as in DP, one all-reduce (SUM) of the step's
+  trainable gradients per step; the loss is scaled by 1 / global batch so the
+  sum equals DP's gradient of the global-batch mean.
+
+Master weights, BN statistics, gradients and optimizer moments are fp32;
+activations are bf16 (throughput) or fp32 (parity) NHWC.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from typing import Dict, List
+
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import MAP_H, MAP_W, Backbone, FrontEnd, _dev
+from .weights import HEAD_LAYOUT, backbone_param_shapes
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+IMG = 512
+FEATURES = 512
+ADAM_BETAS = (0.9, 0.999)
+ADAM_EPS = 1e-8
+WEIGHT_DECAY = 0.01
+MAX_GRAD_NORM = 0.5
+
+
+def block_table():
+    """[(prefix, cin, cout, stride, has_downsample)] of timm resnet18."""
+    out, inp = [], 64
+    for li, planes in enumerate((64, 128, 256, 512)):
+        for b in range(2):
+            s = 2 if (b == 0 and li > 0) else 1
+            out.append((f'layer{li + 1}.{b}', inp, planes, s, b == 0 and li > 0))
+            inp = planes
+    return out
+
+
+BLOCKS = block_table()
+
+
+def param_layout():
+    """[(name, shape)] of the backbone's parameters in timm ``parameters()`` order."""
+    out = []
+    for key, shape, kind in backbone_param_shapes():
+        if kind == 'conv':
+            out.append((f'{key}.weight', shape))
+        else:
+            out.append((f'{key}.weight', shape))
+            out.append((f'{key}.bias', shape))
+    return out
+
+
+def head_keys():
+    """state-dict keys of the trainer's ``model.head`` (``submodel_trainer.py:613-625``)."""
+    keys = []
+    for idx, kind, _ in HEAD_LAYOUT:
+        keys += [f'{idx}.weight', f'{idx}.bias']
+        if kind == 'bn':
+            keys += [f'{idx}.running_mean', f'{idx}.running_var', f'{idx}.num_batches_tracked']
+    return keys
+
+
+# --------------------------------------------------------------- initialisation
+def init_state_dict(seed: int = 42):
+    """Initial trainer model, ``torch.manual_seed(seed)`` then
+    ``timm.create_model('resnet18', pretrained=False, num_classes=0)`` and the
+    MLP head (``submodel_trainer.py:599-625``), reproduced by making the same CPU
+    RNG draws in the same order: every Conv2d/Linear's construction-time
+    ``reset_parameters`` (timm builds a stage's downsample before its blocks),
+    then timm's ``init_weights`` (kaiming_normal_ fan_out / relu on every conv in
+    module order, BN 1/0, ``zero_init_last``: every BasicBlock's bn2.weight = 0).
+    timm is not installed here, so bit-identity with it is unpinned.
+    Returns (backbone_sd, head_sd) with timm / nn.Sequential keys."""
+    g = torch.Generator().manual_seed(seed)
+    layout = backbone_param_shapes()
+    convs = {k: torch.empty(s) for k, s, kind in layout if kind == 'conv'}
+    # construction order: conv1, then per stage: downsample.0, block convs
+    order = ['conv1']
+    for prefix, _, _, _, has_ds in BLOCKS:
+        if has_ds:
+            order.append(f'{prefix}.downsample.0')
+        order += [f'{prefix}.conv1', f'{prefix}.conv2']
+    for k in order:
+        torch.nn.init.kaiming_uniform_(convs[k], a=math.sqrt(5), generator=g)
+    sd = OrderedDict()
+    for k, s, kind in layout:  # named_modules order == state-dict order
+        if kind == 'conv':
+            torch.nn.init.kaiming_normal_(convs[k], mode='fan_out', nonlinearity='relu', generator=g)
+            sd[f'{k}.weight'] = convs[k]
+        else:
+            c = s[0]
+            w = torch.zeros(c) if k.endswith('.bn2') else torch.ones(c)
+            sd[f'{k}.weight'], sd[f'{k}.bias'] = w, torch.zeros(c)
+            sd[f'{k}.running_mean'], sd[f'{k}.running_var'] = torch.zeros(c), torch.ones(c)
+            sd[f'{k}.num_batches_tracked'] = torch.tensor(0, dtype=torch.long)
+    hd = OrderedDict()
+    for idx, kind, shape in HEAD_LAYOUT:
+        if kind == 'linear':  # nn.Linear.reset_parameters
+            w = torch.empty(shape)
+            torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5), generator=g)
+            bound = 1.0 / math.sqrt(shape[1])
+            b = torch.empty(shape[0]).uniform_(-bound, bound, generator=g)
+            hd[f'{idx}.weight'], hd[f'{idx}.bias'] = w, b
+        else:
+            c = shape[0]
+            hd[f'{idx}.weight'], hd[f'{idx}.bias'] = torch.ones(c), torch.zeros(c)
+            hd[f'{idx}.running_mean'], hd[f'{idx}.running_var'] = torch.zeros(c), torch.ones(c)
+            hd[f'{idx}.num_batches_tracked'] = torch.tensor(0, dtype=torch.long)
+    return sd, hd
+
+
+# ------------------------------------------------------------------- front end
+class TrainFrontEnd:
+    """SpectrogramDataset's per-segment transform chain on the device
+    (``submodel_trainer.py:97-114,189-206,463-471``): waveform [n, 128000]
+    fp32 -> image [n, 512, 512] (one of the three identical channels)."""
+
+    def __init__(self, device='cuda', dtype: str = 'bf16'):
+        self.device = _dev(device)
+        self.fe = FrontEnd(self.device, norm=None, top_db=80.0)
+        self.dtype = dtype
+        self._dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
+        self.tdtype = torch.bfloat16 if dtype == 'bf16' else torch.float32
+
+    def maps(self, wave: torch.Tensor, masks: torch.Tensor | None = None) -> torch.Tensor:
+        """standardised maps [n, 128, 251]; masks int32 [n, 4] (f0, f1, t0, t1) or None."""
+        m, db = self.fe(wave, want_db=True)
+        if masks is None:
+            return m
+        masks = masks.to(self.device, torch.int32).contiguous()
+        out = torch.empty_like(m)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_specaug_norm_run', _lib.ptr(db), m.shape[0], MAP_H, MAP_W, _lib.ptr(masks), _lib.ptr(out),
+                      _lib.stream_handle(self.device))
+        return out
+
+    def images(self, maps: torch.Tensor, boxes: torch.Tensor | None = None) -> torch.Tensor:
+        """[n, 512, 512] in the compute dtype; boxes int32 [n, 4] (i, j, h, w) or None."""
+        n = maps.shape[0]
+        img = torch.empty(n, IMG, IMG, device=self.device, dtype=self.tdtype)
+        if boxes is not None:
+            boxes = boxes.to(self.device, torch.int32).contiguous()
+        with torch.cuda.device(self.device):
+            _lib.call('sad_crop_resize_run', _lib.ptr(maps), n, MAP_H, MAP_W, _lib.ptr(boxes), IMG, self._dt,
+                      _lib.ptr(img), _lib.stream_handle(self.device))
+        return img
+
+    def __call__(self, wave, masks=None, boxes=None):
+        return self.images(self.maps(wave, masks), boxes)
+
+
+# ------------------------------------------------------------------- network
+class TrainNet:
+    """timm resnet18 (+ the unused MLP head) in train mode on one device."""
+
+    def __init__(self, base_sd: Dict[str, torch.Tensor], head_sd: Dict[str, torch.Tensor], device='cuda',
+                 dtype: str = 'bf16'):
+        self.device = _dev(device)
+        self.dtype = dtype
+        self._dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
+        self.tdtype = torch.bfloat16 if dtype == 'bf16' else torch.float32
+        self.es = 2 if dtype == 'bf16' else 4
+        layout = param_layout()
+        self.names = [n for n, _ in layout]
+        sizes = [int(np.prod(s)) for _, s in layout]
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        self.offsets = {n: (int(offs[i]), int(offs[i + 1])) for i, n in enumerate(self.names)}
+        total = int(offs[-1])
+        self.pflat = torch.empty(total, device=self.device, dtype=torch.float32)
+        self.gflat = torch.zeros(total, device=self.device, dtype=torch.float32)
+        self.params, self.grads = OrderedDict(), OrderedDict()
+        for (n, s), (a, b) in zip(layout, [self.offsets[n] for n in self.names]):
+            self.params[n] = self.pflat[a:b].view(s)
+            self.grads[n] = self.gflat[a:b].view(s)
+            self.params[n].copy_(torch.as_tensor(base_sd[n], dtype=torch.float32))
+        self.bn_keys = [k for k, _, kind in backbone_param_shapes() if kind == 'bn']
+        self.running = {}
+        self.nbt = {}
+        for k in self.bn_keys:
+            self.running[k] = (torch.as_tensor(base_sd[f'{k}.running_mean'], dtype=torch.float32).to(self.device).clone(),
+                               torch.as_tensor(base_sd[f'{k}.running_var'], dtype=torch.float32).to(self.device).clone())
+            self.nbt[k] = int(torch.as_tensor(base_sd.get(f'{k}.num_batches_tracked', 0)).item())
+        self.head_sd = OrderedDict((k, torch.as_tensor(head_sd[k]).detach().clone().cpu()) for k in head_keys())
+        self.range4 = (self.offsets['layer4.0.conv1.weight'][0], total)
+        self.range3 = (self.offsets['layer3.0.conv1.weight'][0], self.range4[0])
+        self.zero_bias = torch.zeros(FEATURES, device=self.device, dtype=torch.float32)
+        self._packed = {}
+        self._ws = {}
+        self.update_running = True
+
+    # ---------------------------------------------------------- utilities
+    def _stream(self):
+        return _lib.stream_handle(self.device)
+
+    def _buf(self, name: str, nbytes: int) -> torch.Tensor:
+        b = self._ws.get(name)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.device)
+            self._ws[name] = b
+        return b
+
+    def packed(self, conv: str, mode: int) -> torch.Tensor:
+        """Compute-dtype copy of conv weight ``conv`` in pack ``mode`` (cached
+        until the weight changes)."""
+        key = (conv, mode)
+        t = self._packed.get(key)
+        if t is None:
+            w = self.params[f'{conv}.weight']
+            co, ci, k, _ = w.shape
+            n = co * 64 if mode == 2 else w.numel()
+            t = torch.empty(n, device=self.device, dtype=self.tdtype)
+            with torch.cuda.device(self.device):
+                _lib.call('sad_pack_conv_weight_run', _lib.ptr(w), co, ci, k, mode, self._dt, _lib.ptr(t),
+                          self._stream())
+            self._packed[key] = t
+        return t
+
+    def invalidate(self, prefix: str):
+        for key in [k for k in self._packed if k[0].startswith(prefix)]:
+            del self._packed[key]
+
+    def _bn_stats(self, x: torch.Tensor, key: str) -> torch.Tensor:
+        C = x.shape[-1]
+        P = x.numel() // C
+        st = torch.empty(4 * C, device=self.device, dtype=torch.float32)
+        sz = _lib.SZ()
+        _lib.call('sad_bn_workspace_size', P, C, _lib.ctypes.byref(sz))
+        ws = self._buf('bn', sz.value)
+        rm, rv = self.running[key] if self.update_running else (None, None)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_bn_stats_run', _lib.ptr(x), P, C, self._dt, _lib.ptr(self.params[f'{key}.weight']),
+                      _lib.ptr(self.params[f'{key}.bias']), BN_EPS, BN_MOMENTUM, _lib.ptr(rm), _lib.ptr(rv),
+                      _lib.ptr(st), _lib.ptr(ws), ws.numel(), self._stream())
+        if self.update_running:
+            self.nbt[key] += 1
+        return st
+
+    def _bn_apply(self, x, st, res=None, rst=None, relu=True):
+        C = x.shape[-1]
+        out = torch.empty_like(x)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_bn_apply_run', _lib.ptr(x), x.numel() // C, C, self._dt, _lib.ptr(st), _lib.ptr(res),
+                      _lib.ptr(rst), int(relu), _lib.ptr(out), self._stream())
+        return out
+
+    def _conv(self, x, w, cout, k, stride, pad, res=None):
+        """raw NHWC conv (no BN) on the MFMA implicit-GEMM kernel; w packed [cout][k][k][cin]."""
+        N, H, W, Cin = x.shape
+        Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+        out = torch.empty(N, Ho, Wo, cout, device=self.device, dtype=self.tdtype)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_conv2d_run', _lib.ptr(x), N, H, W, Cin, _lib.ptr(w), _lib.ptr(self.zero_bias),
+                      _lib.ptr(res), _lib.ptr(out), cout, k, stride, pad, 0, self._dt, 0, self._stream())
+        return out
+
+    def _bn_backward(self, x, st, key, grads, dy=None, dpool=None, pool_hw=0, y=None, accumulate=False,
+                     want_dz=False):
+        C = x.shape[-1]
+        P = x.numel() // C
+        sz = _lib.SZ()
+        _lib.call('sad_bn_workspace_size', P, C, _lib.ctypes.byref(sz))
+        ws = self._buf('bn', sz.value)
+        dz = torch.empty_like(x) if want_dz else None
+        dx = torch.empty_like(x)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_bn_backward_run', _lib.ptr(x), P, C, self._dt, _lib.ptr(st),
+                      _lib.ptr(self.params[f'{key}.weight']), _lib.ptr(dy), _lib.ptr(dpool), pool_hw, _lib.ptr(y),
+                      _lib.ptr(grads[f'{key}.weight']), _lib.ptr(grads[f'{key}.bias']), int(accumulate),
+                      _lib.ptr(dz), _lib.ptr(dx), _lib.ptr(ws), ws.numel(), self._stream())
+        return dx, dz
+
+    def _wgrad(self, x, dy, key, grads, k, stride, pad, beta=0.0):
+        N, H, W, Cin = x.shape
+        cout = dy.shape[-1]
+        P = dy.numel() // cout
+        need = 0 if (k == 1 and stride == 1 and pad == 0) else P * Cin * k * k * self.es
+        ws = self._buf('col', need)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_conv_wgrad_run', _lib.ptr(x), N, H, W, Cin, _lib.ptr(dy), cout, k, stride, pad, self._dt,
+                      float(beta), _lib.ptr(grads[f'{key}.weight']), _lib.ptr(ws), ws.numel(), self._stream())
+
+    def _dgrad_gemm(self, dy, conv, x_shape, k, stride, pad, dx, accumulate):
+        N, Ho, Wo, cout = dy.shape
+        _, H, W, Cin = x_shape
+        ws = self._buf('dcol', N * Ho * Wo * Cin * k * k * 4)
+        w = self.packed(conv, 3)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_conv_dgrad_run', _lib.ptr(dy), N, Ho, Wo, cout, _lib.ptr(w), Cin, H, W, k, stride, pad,
+                      self._dt, int(accumulate), _lib.ptr(dx), _lib.ptr(ws), ws.numel(), self._stream())
+
+    # ---------------------------------------------------------- forward
+    def forward_train(self, img: torch.Tensor, keep_from: int = 4, stem_chunk: int = 16):
+        """img [B, 512, 512] (compute dtype) -> (pooled features [B, 512] fp32,
+        saved activations of the blocks of layer >= keep_from)."""
+        assert img.dtype == self.tdtype and img.shape[1:] == (IMG, IMG) and img.is_contiguous()
+        B = img.shape[0]
+        s = self._stream()
+        raw = torch.empty(B, 256, 256, 64, device=self.device, dtype=self.tdtype)
+        wst = self.packed('conv1', 2)
+        chunk = max(1, min(B, stem_chunk))
+        col = self._buf('stemcol', chunk * 256 * 256 * 64 * self.es)
+        with torch.cuda.device(self.device):
+            for i in range(0, B, chunk):
+                n = min(chunk, B - i)
+                _lib.call('sad_stem_conv_run', _lib.ptr(img[i:i + n]), n, IMG, IMG, _lib.ptr(wst), _lib.ptr(col),
+                          col.numel(), _lib.ptr(raw[i:i + n]), self._dt, s)
+        st = self._bn_stats(raw, 'bn1')
+        a = torch.empty(B, 128, 128, 64, device=self.device, dtype=self.tdtype)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_bn_relu_maxpool_run', _lib.ptr(raw), B, 256, 256, 64, self._dt, _lib.ptr(st), _lib.ptr(a), s)
+        del raw
+        saved = {}
+        for prefix, cin, cout, stride, has_ds in BLOCKS:
+            c1 = self._conv(a, self.packed(f'{prefix}.conv1', 0), cout, 3, stride, 1)
+            st1 = self._bn_stats(c1, f'{prefix}.bn1')
+            a1 = self._bn_apply(c1, st1, relu=True)
+            c2 = self._conv(a1, self.packed(f'{prefix}.conv2', 0), cout, 3, 1, 1)
+            st2 = self._bn_stats(c2, f'{prefix}.bn2')
+            cd = std = None
+            if has_ds:
+                cd = self._conv(a, self.packed(f'{prefix}.downsample.0', 0), cout, 1, stride, 0)
+                std = self._bn_stats(cd, f'{prefix}.downsample.1')
+                out = self._bn_apply(c2, st2, res=cd, rst=std, relu=True)
+            else:
+                out = self._bn_apply(c2, st2, res=a, relu=True)
+            if int(prefix[5]) >= keep_from:
+                saved[prefix] = dict(x=a, c1=c1, st1=st1, a1=a1, c2=c2, st2=st2, cd=cd, std=std, out=out)
+            a = out
+        feats = torch.empty(B, FEATURES, device=self.device, dtype=torch.float32)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_avgpool_run', _lib.ptr(a), B, a.shape[1] * a.shape[2], FEATURES, self._dt,
+                      _lib.ptr(feats), s)
+        return feats, saved
+
+    # ---------------------------------------------------------- backward
+    def backward(self, dfeat: torch.Tensor, saved: dict, layers=(4,), grads3: Dict[str, torch.Tensor] | None = None):
+        """Gradients of the trainable stages from d(loss)/d(features):
+        layer4 into ``self.grads`` (overwritten, as after zero_grad), layer3 (if
+        3 in layers) into ``grads3`` (overwritten; the caller folds them into the
+        accumulating .grad, quirk C4)."""
+        order = [b for b in reversed(BLOCKS) if int(b[0][5]) in layers]
+        dy, dpool = None, dfeat
+        for bi, (prefix, cin, cout, stride, has_ds) in enumerate(order):
+            sv = saved[prefix]
+            G = self.grads if prefix.startswith('layer4') else grads3
+            Ho = sv['c2'].shape[1]
+            dc2, dz2 = self._bn_backward(sv['c2'], sv['st2'], f'{prefix}.bn2', G, dy=dy, dpool=dpool,
+                                         pool_hw=Ho * Ho if dpool is not None else 0, y=sv['out'], want_dz=True)
+            dcd = None
+            if has_ds:
+                dcd, _ = self._bn_backward(sv['cd'], sv['std'], f'{prefix}.downsample.1', G, dy=dz2)
+                self._wgrad(sv['x'], dcd, f'{prefix}.downsample.0', G, 1, stride, 0)
+            self._wgrad(sv['a1'], dc2, f'{prefix}.conv2', G, 3, 1, 1)
+            da1 = self._conv(dc2, self.packed(f'{prefix}.conv2', 1), cout, 3, 1, 1)
+            dc1, _ = self._bn_backward(sv['c1'], sv['st1'], f'{prefix}.bn1', G, dy=da1, y=sv['a1'])
+            self._wgrad(sv['x'], dc1, f'{prefix}.conv1', G, 3, stride, 1)
+            if bi + 1 == len(order):
+                break
+            if stride == 1:
+                dx = self._conv(dc1, self.packed(f'{prefix}.conv1', 1), cin, 3, 1, 1, res=dz2)
+            else:
+                dx = torch.empty_like(sv['x'])
+                self._dgrad_gemm(dc1, f'{prefix}.conv1', sv['x'].shape, 3, stride, 1, dx, False)
+                self._dgrad_gemm(dcd, f'{prefix}.downsample.0', sv['x'].shape, 1, stride, 0, dx, True)
+            dy, dpool = dx, None
+
+    # ---------------------------------------------------------- optimizer
+    def clip_grad_norm(self, lo: int, hi: int, max_norm: float = MAX_GRAD_NORM) -> torch.Tensor:
+        """clip_grad_norm_ over gflat[lo:hi]; returns device [norm, coef]."""
+        nc = torch.empty(2, device=self.device, dtype=torch.float32)
+        ws = self._buf('clip', 1024 * 8)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_clip_grad_norm_run', _lib.ptr(self.gflat[lo:hi]), hi - lo, float(max_norm), _lib.ptr(nc),
+                      _lib.ptr(ws), ws.numel(), self._stream())
+        return nc
+
+    # ---------------------------------------------------------- eval / export
+    def base_state_dict(self) -> "OrderedDict[str, torch.Tensor]":
+        """timm-keyed backbone state dict (CPU), parameters + BN buffers."""
+        sd = OrderedDict()
+        for key, shape, kind in backbone_param_shapes():
+            if kind == 'conv':
+                sd[f'{key}.weight'] = self.params[f'{key}.weight'].detach().cpu().clone()
+            else:
+                sd[f'{key}.weight'] = self.params[f'{key}.weight'].detach().cpu().clone()
+                sd[f'{key}.bias'] = self.params[f'{key}.bias'].detach().cpu().clone()
+                rm, rv = self.running[key]
+                sd[f'{key}.running_mean'] = rm.cpu().clone()
+                sd[f'{key}.running_var'] = rv.cpu().clone()
+                sd[f'{key}.num_batches_tracked'] = torch.tensor(self.nbt[key], dtype=torch.long)
+        return sd
+
+    def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
+        """``get_model(model).state_dict()`` of the reference trainer: timm keys,
+        then ``head.*`` (submodel_trainer.py:706)."""
+        sd = self.base_state_dict()
+        for k, v in self.head_sd.items():
+            sd[f'head.{k}'] = v.clone()
+        return sd
+
+    def eval_backbone(self, micro_batch: int = 64) -> Backbone:
+        """``model.eval()`` forward: the inference plan (BN folded with the
+        current running statistics)."""
+        return Backbone(self.base_state_dict(), self.device, self.dtype, micro_batch)
+
+
+def ce_loss(feats: torch.Tensor, targets: torch.Tensor, scale: float = 0.0, want_grad: bool = False,
+            want_pred: bool = False):
+    """(dlogits or None, device [loss_sum, n_correct][, argmax int32 [B]]) of
+    CrossEntropyLoss on ``feats`` [B, C] with int64 ``targets`` [B]."""
+    B, C = feats.shape
+    out = torch.empty(2, device=feats.device, dtype=torch.float32)
+    d = torch.empty_like(feats)
+    pred = torch.empty(B, device=feats.device, dtype=torch.int32) if want_pred else None
+    t = targets.to(feats.device, torch.int64).contiguous()
+    with torch.cuda.device(feats.device):
+        _lib.call('sad_ce_loss_run', _lib.ptr(feats), _lib.ptr(t), B, C, float(scale), _lib.ptr(d), _lib.ptr(out),
+                  _lib.ptr(pred), _lib.stream_handle(feats.device))
+    if want_pred:
+        return (d if want_grad else None), out, pred
+    return (d if want_grad else None), out
+
+
+class Trainer:
+    """One trainer replica: TrainNet + AdamW/clip state + the C4 layer3 gradient
+    accumulator, with an optional process group (DDP over RCCL)."""
+
+    def __init__(self, base_sd, head_sd, device='cuda', dtype: str = 'bf16', lr: float = 1e-3, group=None,
+                 world: int = 1):
+        self.net = TrainNet(base_sd, head_sd, device, dtype)
+        self.device = self.net.device
+        self.group, self.world = group, world
+        a4, b4 = self.net.range4
+        self.m = torch.zeros(b4 - a4, device=self.device, dtype=torch.float32)
+        self.v = torch.zeros_like(self.m)
+        self.step_count = 0
+        self.lr = lr
+        self.layer3_unfrozen = False
+        self.grads3 = None
+        self._g3flat = None
+        # torch.optim.AdamW over the same parameter list as the reference
+        # (filter(requires_grad): layer4 then head, submodel_trainer.py:648-652) -- used
+        # only for state_dict()/load_state_dict() and ReduceLROnPlateau; its step()
+        # is never called (sad_adamw_run is the step).
+        l4 = [n for n in self.net.names if n.startswith('layer4.')]
+        self.l4_names = l4
+        self._head_params = [torch.nn.Parameter(self.net.head_sd[k].clone().float())
+                             for k in head_keys() if not k.endswith(('running_mean', 'running_var',
+                                                                     'num_batches_tracked'))]
+        self._l4_params = [torch.nn.Parameter(self.net.params[n].detach().cpu().clone()) for n in l4]
+        self.optimizer = torch.optim.AdamW(self._l4_params + self._head_params, lr=lr, weight_decay=WEIGHT_DECAY)
+
+    # reference: for p in layer3.parameters(): p.requires_grad = True  (:687-691)
+    def unfreeze_layer3(self):
+        if self.layer3_unfrozen:
+            return
+        self.layer3_unfrozen = True
+        a3, b3 = self.net.range3
+        self.net.gflat[a3:b3].zero_()
+        self._g3flat = torch.empty(b3 - a3, device=self.device, dtype=torch.float32)
+        self.grads3 = OrderedDict()
+        for n in self.net.names:
+            if n.startswith('layer3.'):
+                lo, hi = self.net.offsets[n]
+                self.grads3[n] = self._g3flat[lo - a3:hi - a3].view(self.net.params[n].shape)
+
+    @property
+    def current_lr(self) -> float:
+        return float(self.optimizer.param_groups[-1]['lr'])
+
+    def train_step(self, img: torch.Tensor, targets: torch.Tensor, global_batch: int | None = None):
+        """One iteration of submodel_trainer.train()'s batch loop (:253-293).
+        ``global_batch`` = rows over all ranks (summed with an all-reduce if
+        None).  Returns (mean loss over the global batch, correct count, global
+        rows, stepped?)."""
+        net = self.net
+        if global_batch is None:
+            global_batch = img.shape[0]
+            if self.world > 1:
+                import torch.distributed as dist
+                t = torch.tensor([global_batch], device=self.device, dtype=torch.int64)
+                dist.all_reduce(t, group=self.group)
+                global_batch = int(t.item())
+        layers = (3, 4) if self.layer3_unfrozen else (4,)
+        feats, saved = net.forward_train(img, keep_from=min(layers))
+        dfeat, lc = ce_loss(feats, targets, 1.0 / global_batch, want_grad=True)
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(lc, group=self.group)
+        loss_sum, correct = lc.tolist()
+        loss = loss_sum / global_batch
+        if not math.isfinite(loss):  # NaN/Inf: skip the step (:266-271)
+            return loss, 0, 0, False
+        net.backward(dfeat, saved, layers, self.grads3)
+        a4, b4 = net.range4
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(net.gflat[a4:b4], group=self.group)
+            if self.layer3_unfrozen:
+                dist.all_reduce(self._g3flat, group=self.group)
+        lo = a4
+        if self.layer3_unfrozen:
+            a3, b3 = net.range3
+            with torch.cuda.device(self.device):
+                _lib.call('sad_axpy_run', _lib.ptr(net.gflat[a3:b3]), _lib.ptr(self._g3flat), b3 - a3, 1.0,
+                          _lib.stream_handle(self.device))
+            lo = a3
+        self.last_norm = net.clip_grad_norm(lo, b4)
+        self.step_count += 1
+        lr = self.current_lr
+        with torch.cuda.device(self.device):
+            _lib.call('sad_adamw_run', _lib.ptr(net.pflat[a4:b4]), _lib.ptr(net.gflat[a4:b4]), _lib.ptr(self.m),
+                      _lib.ptr(self.v), b4 - a4, lr, ADAM_BETAS[0], ADAM_BETAS[1], ADAM_EPS, WEIGHT_DECAY,
+                      self.step_count, _lib.stream_handle(self.device))
+        net.invalidate('layer4.')
+        return loss, int(correct), int(global_batch), True
+
+    # ------------------------------------------------------------ checkpoints
+    def optimizer_state_dict(self) -> dict:
+        a4, _ = self.net.range4
+        st = {}
+        if self.step_count:
+            for i, n in enumerate(self.l4_names):
+                lo, hi = self.net.offsets[n]
+                shp = self.net.params[n].shape
+                st[i] = {'step': torch.tensor(float(self.step_count)),
+                         'exp_avg': self.m[lo - a4:hi - a4].view(shp).cpu().clone(),
+                         'exp_avg_sq': self.v[lo - a4:hi - a4].view(shp).cpu().clone()}
+        sd = self.optimizer.state_dict()
+        sd['state'] = st
+        return sd
+
+    def load_optimizer_state_dict(self, sd: dict):
+        self.optimizer.load_state_dict(sd)
+        a4, _ = self.net.range4
+        steps = []
+        for i, n in enumerate(self.l4_names):
+            s = sd['state'].get(i)
+            if not s:
+                continue
+            lo, hi = self.net.offsets[n]
+            self.m[lo - a4:hi - a4].copy_(torch.as_tensor(s['exp_avg']).reshape(-1))
+            self.v[lo - a4:hi - a4].copy_(torch.as_tensor(s['exp_avg_sq']).reshape(-1))
+            steps.append(int(float(torch.as_tensor(s['step']).item())))
+        self.step_count = max(steps) if steps else 0
+        self.optimizer.state.clear()
+
+    def load_state_dict(self, sd: dict):
+        """``get_model(model).load_state_dict(state_dict)`` (strict) of a trainer checkpoint."""
+        net = self.net
+        for n in net.names:
+            net.params[n].copy_(torch.as_tensor(sd[n], dtype=torch.float32))
+        for k in net.bn_keys:
+            net.running[k][0].copy_(torch.as_tensor(sd[f'{k}.running_mean']))
+            net.running[k][1].copy_(torch.as_tensor(sd[f'{k}.running_var']))
+            net.nbt[k] = int(torch.as_tensor(sd[f'{k}.num_batches_tracked']).item())
+        for k in head_keys():
+            net.head_sd[k] = torch.as_tensor(sd[f'head.{k}']).clone()
+        net._packed.clear()

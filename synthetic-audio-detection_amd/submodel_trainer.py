@@ -1,0 +1,530 @@
+#!/usr/bin/env python3
+"""Drop-in replacement for the reference's ``modular/source/submodel_trainer.py``
+on MI355X: same CLI flags and defaults, same module symbols, same checkpoint
+format (``model_best.pth``: epoch / state_dict / best_acc / optimizer /
+scheduler / total_steps); the device work runs on libsad (HIP, gfx950) through
+``sad.train``.
+
+Reference map (file:line in modular/source/submodel_trainer.py):
+  parse_args / setup_logging     :33-66
+  SpectrogramDataset             :69-218  -> file discovery, WAV load, resample and
+                                             the 2-segment rules on the host; the
+                                             spectrogram chain runs on the device
+  custom_collate_fn              :221-238
+  train / validate / evaluate    :241-460
+  get_dataloaders                :463-511
+  initialize_weights, get_model  :514-528
+  main                           :531-727
+
+Behaviour kept on purpose: the attached head is never
+used, the loss is CrossEntropy over the 512 pooled features (C1); layer3 is
+unfrozen at epochs//3 but never optimised, its gradients accumulate and enter
+the clip norm (C4); mel norm=None (C3); the epoch loss divides the sum of
+loss*2B by the number of FILES (:285,304).
+
+Differences (documented in DESIGN.md / INTEGRATION.md):
+  * ``SpectrogramDataset.__getitem__`` returns the two fp32 waveform segments
+    and their drawn augmentation parameters instead of finished [3,512,512]
+    images: ``(seg1 [128000], target, seg2 [128000], target, aug int32 [2, 8])``
+    with aug[k] = (f0, f1, t0, t1, i, j, h, w).  The device builds the images.
+  * ``--num_gpus > 1`` = one process per GPU (torchrun) over RCCL instead of
+    DataParallel threads: each rank loads ``--batch-size`` files per step;
+    per-replica BN statistics as in DP; gradients all-reduced.
+  * no CPU fallback; ``--model-name`` must be resnet18 (the device kernels
+    implement timm's BasicBlock resnet18, the only backbone inference uses).
+  * extra flags: ``--precision {bf16,fp32}`` (default bf16 = throughput mode),
+    ``--max-steps`` (stop an epoch early; benchmarking).
+  * TensorBoard is optional (not installed here): scalars are logged instead.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import random
+import sys
+import warnings
+from datetime import datetime
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader, Dataset
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if _HERE not in sys.path:
+    sys.path.insert(0, _HERE)
+
+from sad import audio as _audio  # noqa: E402
+from sad import augment as _augment  # noqa: E402
+
+warnings.filterwarnings("ignore")
+
+SEGMENT_LENGTH = 4 * 32000
+# timm.list_models('resnet*') is unavailable offline: the choices the reference's
+# CLI accepts for --model-name (timm 0.9 names); only resnet18 runs on the device.
+RESNET_MODELS = ['resnet10t', 'resnet14t', 'resnet18', 'resnet18d', 'resnet26', 'resnet26d', 'resnet26t',
+                 'resnet32ts', 'resnet33ts', 'resnet34', 'resnet34d', 'resnet50', 'resnet50_gn', 'resnet50d',
+                 'resnet50t', 'resnet51q', 'resnet61q', 'resnet101', 'resnet101d', 'resnet152', 'resnet152d',
+                 'resnet200', 'resnet200d']
+
+
+def parse_args(argv=None):
+    """Parses command-line arguments (:33-53)."""
+    parser = argparse.ArgumentParser(description='Audio Classification Training')
+    parser.add_argument('--data-dir', default='./dataset', type=str, help='Path to dataset')
+    parser.add_argument('--batch-size', default=32, type=int, help='Batch size per GPU')
+    parser.add_argument('--epochs', default=100, type=int, help='Number of total epochs to run')
+    parser.add_argument('--lr', default=0.001, type=float, help='Initial learning rate')
+    parser.add_argument('--workers', default=20, type=int, help='Number of data loading workers')
+    parser.add_argument('--seed', default=42, type=int, help='Seed for initializing training.')
+    parser.add_argument('--gpu', default=0, type=int, help='GPU id to use.')
+    parser.add_argument('--num_gpus', default=1, type=int, help='Number of GPUs to use')
+    parser.add_argument('--checkpoint-dir', default='./checkpoints', type=str, help='Directory to save checkpoints')
+    parser.add_argument('--resume', default='', type=str, help='Path to resume checkpoint')
+    parser.add_argument('--evaluate', dest='evaluate', action='store_true', help='Evaluate model on validation set')
+    parser.add_argument('--Class0', default='Real', type=str, help='Name of Class 0 eg. Real')
+    parser.add_argument('--Class1', default='Class1', type=str, help='Name of Class 1 eg. Training platform')
+    parser.add_argument('--model-name', default='resnet18', type=str, choices=RESNET_MODELS,
+                        help='Name of model to use')
+    parser.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'],
+                        help='device compute precision (fp32 = the reference arithmetic)')
+    parser.add_argument('--max-steps', default=0, type=int, help='stop each epoch after this many steps (0 = all)')
+    return parser.parse_args(argv)
+
+
+def setup_logging():
+    """Sets up logging configuration (:56-66)."""
+    os.makedirs('logs', exist_ok=True)
+    logging.basicConfig(
+        filename=f'logs/training_{datetime.now().strftime("%Y%m%d-%H%M%S")}.log',
+        level=logging.INFO,
+        format='%(asctime)s %(message)s',
+    )
+    console = logging.StreamHandler()
+    console.setLevel(logging.INFO)
+    logging.getLogger('').addHandler(console)
+
+
+def segment_waveform(waveform: torch.Tensor, min_length_ratio: float = 0.9):
+    """The two training segments of one file (:155-187), or None if too short."""
+    seg = SEGMENT_LENGTH
+    n = waveform.size(1)
+    if n >= 2 * seg:
+        return [waveform[:, :seg], waveform[:, seg:2 * seg]]
+    if n >= seg:
+        first = waveform[:, :seg]
+        return [first, first]
+    if n >= seg * min_length_ratio:
+        padded = torch.nn.functional.pad(waveform, (0, seg - n), mode='constant', value=0)
+        return [padded, padded]
+    return None
+
+
+class SpectrogramDataset(Dataset):
+    """Dataset of 2-segment training samples (:69-218); see the module docstring
+    for what __getitem__ returns."""
+
+    def __init__(self, data_dir, mode, transform=None, class_names=None):
+        self.mode = mode
+        # 'train' -> RandomResizedCrop(512, scale=(0.8, 1.0)) (:465-467); anything else
+        # (the val transform Resize((512,512)), :469-471) -> the full image.
+        self.transform = transform
+        self.classes = ['Real', 'Class1'] if class_names is None else class_names
+        self.class_to_idx = {cls_name: i for i, cls_name in enumerate(self.classes)}
+        self.samples = self._make_dataset(data_dir)
+        logging.info(f"Found {len(self.samples)} samples for mode {self.mode}")
+        logging.info(f"Classes: {self.classes}")
+        logging.info(f"Class-to-Index Mapping: {self.class_to_idx}")
+        self.augment = self.mode == 'train'
+        self.min_length_ratio = 0.9
+
+    def _make_dataset(self, directory):
+        """(path, class index) for every .wav under <dir>/<mode>/<class>/ (:118-137)."""
+        instances = []
+        for target_class in self.classes:
+            class_index = self.class_to_idx[target_class]
+            target_dir = os.path.join(directory, self.mode, target_class)
+            if not os.path.isdir(target_dir):
+                logging.warning(f"Directory {target_dir} does not exist. Skipping.")
+                continue
+            for root, _, fnames in sorted(os.walk(target_dir)):
+                for fname in sorted(fnames):
+                    if fname.endswith('.wav'):
+                        instances.append((os.path.join(root, fname), class_index))
+        if not instances:
+            raise RuntimeError(f"No wav files found in {directory}/{self.mode}")
+        return instances
+
+    def _aug_params(self):
+        """Per segment, in the reference's RNG order (:190-206): the SpecAugment
+        masks, then self.transform's RandomResizedCrop parameters."""
+        rows = []
+        for _ in range(2):
+            mask = _augment.specaug_masks() if self.augment else _augment.NO_MASK
+            box = _augment.random_resized_crop_params() if self.transform == 'train' else _augment.FULL_IMAGE
+            rows.append(list(mask) + list(box))
+        return torch.tensor(rows, dtype=torch.int32)
+
+    def __getitem__(self, index):
+        path, target = self.samples[index]
+        try:
+            waveform, sample_rate = _audio.load(path)
+            if waveform.numel() == 0:
+                logging.debug(f"Empty waveform detected at index {index} for path {path}")
+                return None
+            if sample_rate != 32000:
+                waveform = _audio.resample(waveform, sample_rate, 32000)
+            if waveform.size(0) != 1:
+                # the reference would build a [2C,...] image that the 3-channel model rejects
+                raise ValueError(f'expected mono audio, got {waveform.size(0)} channels')
+            segs = segment_waveform(waveform, self.min_length_ratio)
+            if segs is None:
+                logging.debug(f"File too short at index {index}, path {path}. Length: {waveform.size(1)}, "
+                              f"Required: {2 * SEGMENT_LENGTH}")
+                return None
+            aug = self._aug_params()
+            return segs[0][0].contiguous(), target, segs[1][0].contiguous(), target, aug
+        except Exception as e:
+            logging.warning(f"Error processing file at index {index}, path {path}: {str(e)}")
+            return None
+
+    def __len__(self):
+        return len(self.samples)
+
+
+def custom_collate_fn(batch):
+    """Drops None samples (:221-238); returns (wave1 [B,T], target1, wave2,
+    target2, aug [B,2,8]) or None."""
+    batch = list(filter(lambda x: x is not None, batch))
+    if len(batch) == 0:
+        return None
+    input1, target1, input2, target2, aug = zip(*batch)
+    return (torch.stack(input1), torch.tensor(target1), torch.stack(input2), torch.tensor(target2),
+            torch.stack(aug))
+
+
+class _Scalars:
+    """Stand-in for torch.utils.tensorboard.SummaryWriter (tensorboard absent)."""
+
+    def __init__(self, log_dir=None):
+        self.log_dir = log_dir
+
+    def add_scalar(self, tag, value, step):
+        logging.debug(f'{tag} {value} @ {step}')
+
+    def close(self):
+        pass
+
+
+def _summary_writer(log_dir):
+    try:
+        from torch.utils.tensorboard import SummaryWriter
+        return SummaryWriter(log_dir=log_dir)
+    except Exception:
+        return _Scalars(log_dir)
+
+
+class DeviceModel:
+    """What the reference's ``model`` object is to train()/validate(): the
+    device trainer + front end, rank/world of this process."""
+
+    def __init__(self, trainer, frontend, rank=0, world=1, group=None):
+        self.trainer, self.frontend = trainer, frontend
+        self.rank, self.world, self.group = rank, world, group
+
+    def images(self, batch, train: bool):
+        input1, target1, input2, target2, aug = batch
+        dev = self.trainer.device
+        waves = torch.cat((input1, input2), dim=0).to(dev, non_blocking=True)
+        targets = torch.cat((target1, target2), dim=0)
+        aug = torch.cat((aug[:, 0], aug[:, 1]), dim=0)
+        masks = aug[:, :4] if train else None
+        boxes = aug[:, 4:] if train else None
+        return self.frontend(waves, masks, boxes), targets
+
+    def maps(self, batch):
+        input1, target1, input2, target2, _ = batch
+        waves = torch.cat((input1, input2), dim=0).to(self.trainer.device, non_blocking=True)
+        return self.frontend.maps(waves), torch.cat((target1, target2), dim=0)
+
+
+def _allreduce_sum(values, model):
+    if model.world <= 1:
+        return values
+    import torch.distributed as dist
+    t = torch.tensor(values, dtype=torch.float64, device=model.trainer.device)
+    dist.all_reduce(t, group=model.group)
+    return t.tolist()
+
+
+def train(args, train_loader, model, criterion, optimizer, scheduler, epoch, writer, total_steps, device):
+    """Performs one epoch of training (:241-313)."""
+    running_loss = 0.0
+    correct = 0
+    total = 0
+    tr = model.trainer
+    n_files = len(train_loader.dataset)
+    for batch_idx, batch in enumerate(train_loader):
+        if args.max_steps and batch_idx >= args.max_steps:
+            break
+        if batch is None:
+            continue
+        try:
+            img, targets = model.images(batch, train=True)
+            loss, corr, rows, ok = tr.train_step(img, targets)
+            if not ok:
+                logging.warning(f'NaN or Inf loss encountered at epoch {epoch}, batch {batch_idx}, skipping step.')
+                continue
+            total += rows
+            correct += corr
+            running_loss += loss * rows
+            total_steps += 1
+            if batch_idx % 10 == 0 and model.rank == 0:
+                logging.info(f"Epoch [{epoch}] batch {batch_idx}: loss={loss:.4f} acc={100. * correct / total:.2f}% "
+                             f"lr={tr.current_lr:.6f}")
+            if total_steps % 100 == 0:
+                writer.add_scalar('Loss/train_step', loss, total_steps)
+                writer.add_scalar('Accuracy/train_step', 100. * correct / total, total_steps)
+                writer.add_scalar('Learning_rate', tr.current_lr, total_steps)
+        except Exception as e:
+            logging.error(f'Error in training batch {batch_idx}: {str(e)}')
+            continue
+    # the reference divides by the dataset's file count (each file gave 2 rows, :285,304)
+    n_total_files = n_files
+    epoch_loss = running_loss / n_total_files if n_total_files > 0 else 0.0
+    epoch_acc = 100. * correct / total if total > 0 else 0.0
+    if isinstance(scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
+        scheduler.step(epoch_loss)
+    else:
+        scheduler.step()
+    return epoch_loss, epoch_acc, total_steps
+
+
+def _eval_pass(val_loader, model):
+    """model.eval() pass: BN folded with the running statistics (the inference
+    plan), CE + argmax on the pooled features.  Returns (loss_sum, correct,
+    total, predictions, targets) summed over ranks (lists from this rank)."""
+    bb = model.trainer.net.eval_backbone()
+    from sad.train import ce_loss
+    loss_sum = 0.0
+    correct = total = 0
+    preds, tgts = [], []
+    for batch in val_loader:
+        if batch is None:
+            continue
+        maps, targets = model.maps(batch)
+        feats = bb(maps)
+        _, lc, pred = ce_loss(feats, targets, want_pred=True)
+        ls, c = lc.tolist()
+        loss_sum += ls
+        correct += int(c)
+        total += targets.numel()
+        preds.extend(pred.cpu().numpy().tolist())
+        tgts.extend(targets.numpy().tolist())
+    loss_sum, correct, total = _allreduce_sum([loss_sum, correct, total], model)
+    if model.world > 1:
+        import torch.distributed as dist
+        gp, gt = [None] * model.world, [None] * model.world
+        dist.all_gather_object(gp, preds, group=model.group)
+        dist.all_gather_object(gt, tgts, group=model.group)
+        preds = [p for r in gp for p in r]
+        tgts = [t for r in gt for t in r]
+    return loss_sum, int(correct), int(total), preds, tgts
+
+
+def validate(args, val_loader, model, criterion, epoch, device):
+    """Performs one epoch of validation (:316-385)."""
+    classes = val_loader.dataset.classes
+    loss_sum, correct, total, preds, tgts = _eval_pass(val_loader, model)
+    preds = [min(max(p, 0), len(classes) - 1) for p in preds]  # :349
+    epoch_loss = loss_sum / len(val_loader.dataset) if len(val_loader.dataset) > 0 else 0.0
+    epoch_acc = 100. * correct / total if total > 0 else 0.0
+    logging.info(f"Unique targets in validation: {set(tgts)}")
+    logging.info(f"Unique predictions in validation: {set(preds)}")
+    try:
+        from sklearn.metrics import classification_report
+        report = classification_report(tgts, preds, target_names=classes, labels=list(range(len(classes))))
+        logging.info(f"\nClassification Report:\n{report}")
+    except Exception as e:  # sklearn is reporting only
+        logging.info(f'classification report unavailable: {e}')
+    return epoch_loss, epoch_acc, preds, tgts
+
+
+def evaluate(args, model, val_loader, criterion, device):
+    """Detailed metrics on the validation set (:388-460)."""
+    classes = [args.Class0, args.Class1]
+    _, _, _, preds, tgts = _eval_pass(val_loader, model)
+    class_correct = [0] * 5
+    class_total = [0] * 5
+    logging.info("Starting evaluation...")
+    for p, t in zip(preds, tgts):
+        if t < len(classes):
+            class_correct[t] += int(p == t)
+            class_total[t] += 1
+    accuracy = 100 * sum(class_correct) / sum(class_total) if sum(class_total) > 0 else 0.0
+    logging.info("\nEvaluation Results:")
+    logging.info(f"Overall Accuracy: {accuracy:.2f}%\n")
+    logging.info("Per-class Accuracy:")
+    for i in range(len(classes)):
+        if class_total[i] > 0:
+            logging.info(f"{classes[i]}: {100 * class_correct[i] / class_total[i]:.2f}% "
+                         f"({int(class_correct[i])}/{class_total[i]})")
+        else:
+            logging.info(f"{classes[i]}: No samples.")
+    from sklearn.metrics import classification_report, confusion_matrix
+    cm = confusion_matrix(tgts, preds, labels=list(range(len(classes))))
+    report = classification_report(tgts, preds, target_names=classes, labels=list(range(len(classes))))
+    logging.info("\nConfusion Matrix:")
+    logging.info(f"{cm}")
+    logging.info("\nDetailed Classification Report:")
+    logging.info(report)
+    return accuracy, cm
+
+
+def get_dataloaders(args, rank: int = 0, world: int = 1):
+    """Creates data loaders for training and validation (:463-511).  With
+    world > 1 each rank reads a disjoint shard (DistributedSampler) of
+    ``--batch-size`` files per step."""
+    train_dataset = SpectrogramDataset(args.data_dir, 'train', transform='train',
+                                       class_names=[args.Class0, args.Class1])
+    val_dataset = SpectrogramDataset(args.data_dir, 'test', transform='val',
+                                     class_names=[args.Class0, args.Class1])
+    per_rank = args.batch_size if world > 1 else (args.batch_size * args.num_gpus if args.num_gpus > 0
+                                                   else args.batch_size)
+    logging.info(f"Total batch size: {per_rank * world}")
+    tsamp = vsamp = None
+    if world > 1:
+        from torch.utils.data.distributed import DistributedSampler
+        tsamp = DistributedSampler(train_dataset, num_replicas=world, rank=rank, shuffle=True, seed=args.seed)
+        vsamp = DistributedSampler(val_dataset, num_replicas=world, rank=rank, shuffle=False)
+    train_loader = DataLoader(train_dataset, batch_size=per_rank, num_workers=args.workers, pin_memory=True,
+                              shuffle=tsamp is None, sampler=tsamp, drop_last=False, collate_fn=custom_collate_fn)
+    val_loader = DataLoader(val_dataset, batch_size=per_rank, num_workers=args.workers, pin_memory=True,
+                            shuffle=False, sampler=vsamp, drop_last=False, collate_fn=custom_collate_fn)
+    return train_loader, val_loader
+
+
+def initialize_weights(model):
+    """(:514-520) kept for API parity; the reference never calls it."""
+    import torch.nn as nn
+    import torch.nn.init as init
+    for module in model.modules():
+        if isinstance(module, (nn.Conv2d, nn.Linear)):
+            init.kaiming_normal_(module.weight)
+            if module.bias is not None:
+                init.constant_(module.bias, 0)
+
+
+def get_model(model):
+    """(:523-528): the underlying model object."""
+    return getattr(model, 'module', model)
+
+
+def save_checkpoint(path, epoch, trainer, scheduler, best_acc, total_steps):
+    """model_best.pth in the reference's format (:704-714)."""
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    torch.save({
+        'epoch': epoch,
+        'state_dict': trainer.net.state_dict(),
+        'best_acc': best_acc,
+        'optimizer': trainer.optimizer_state_dict(),
+        'scheduler': scheduler.state_dict(),
+        'total_steps': total_steps,
+    }, path)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    setup_logging()
+    logging.info(f"Arguments: {args}")
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world == 1 and args.num_gpus > torch.cuda.device_count():
+        logging.error(f"Requested number of GPUs ({args.num_gpus}) is greater than available GPUs "
+                      f"({torch.cuda.device_count()})")
+        sys.exit(1)
+    if args.model_name != 'resnet18':
+        raise NotImplementedError(f'--model-name {args.model_name}: the MI355X kernels implement resnet18 only')
+    if not torch.cuda.is_available():
+        raise RuntimeError('submodel_trainer runs on MI355X GPUs only (no CPU path)')
+    torch.cuda.set_device(local)
+    device = torch.device('cuda', local)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=device)
+        group = dist.group.WORLD
+    logging.info(f"Using device: {device}; ranks: {world}")
+
+    torch.manual_seed(args.seed)
+    torch.cuda.manual_seed(args.seed)
+    np.random.seed(args.seed)
+    random.seed(args.seed)
+
+    from sad import train as st
+    logging.info("Creating model with RANDOM weights...")
+    base_sd, head_sd = st.init_state_dict(args.seed)
+    trainer = st.Trainer(base_sd, head_sd, device, args.precision, lr=args.lr, group=group, world=world)
+    frontend = st.TrainFrontEnd(device, args.precision)
+    model = DeviceModel(trainer, frontend, rank, world, group)
+
+    train_loader, val_loader = get_dataloaders(args, rank, world)
+    logging.info(f"Number of training samples: {len(train_loader.dataset)}")
+    logging.info(f"Number of validation samples: {len(val_loader.dataset)}")
+    optimizer = trainer.optimizer
+    scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode='min', factor=0.5, patience=2)
+    writer = _summary_writer(f'runs/experiment_{datetime.now().strftime("%Y%m%d-%H%M%S")}')
+
+    best_acc = 0.0
+    total_steps = 0
+    start_epoch = 0
+    if args.resume:
+        if os.path.isfile(args.resume):
+            logging.info(f"Loading checkpoint '{args.resume}'")
+            checkpoint = torch.load(args.resume, map_location='cpu', weights_only=True)
+            trainer.load_state_dict(checkpoint['state_dict'])
+            trainer.load_optimizer_state_dict(checkpoint['optimizer'])
+            scheduler.load_state_dict(checkpoint['scheduler'])
+            start_epoch = checkpoint['epoch'] + 1
+            best_acc = checkpoint['best_acc']
+            total_steps = checkpoint.get('total_steps', 0)
+            logging.info(f"Loaded checkpoint '{args.resume}' (epoch {checkpoint['epoch']})")
+        else:
+            logging.error(f"No checkpoint found at '{args.resume}'")
+
+    for epoch in range(start_epoch, args.epochs):
+        logging.info(f'\nEpoch: {epoch}/{args.epochs - 1}')
+        if epoch == args.epochs // 3:
+            logging.info("Unfreezing more layers...")
+            trainer.unfreeze_layer3()
+        if world > 1 and hasattr(train_loader.sampler, 'set_epoch'):
+            train_loader.sampler.set_epoch(epoch)
+        train_loss, train_acc, total_steps = train(args, train_loader, model, None, optimizer, scheduler, epoch,
+                                                   writer, total_steps, device)
+        val_loss, val_acc, _, _ = validate(args, val_loader, model, None, epoch, device)
+        logging.info(f'epoch {epoch}: train loss {train_loss:.4f} acc {train_acc:.2f}% | '
+                     f'val loss {val_loss:.4f} acc {val_acc:.2f}%')
+        is_best = val_acc > best_acc
+        best_acc = max(val_acc, best_acc)
+        if is_best and rank == 0:
+            save_checkpoint(os.path.join(args.checkpoint_dir, 'model_best.pth'), epoch, trainer, scheduler,
+                            best_acc, total_steps)
+            logging.info(f'Saved best model with accuracy: {val_acc:.2f}%')
+        writer.add_scalar('Loss/train_epoch', train_loss, epoch)
+        writer.add_scalar('Accuracy/train_epoch', train_acc, epoch)
+        writer.add_scalar('Loss/val_epoch', val_loss, epoch)
+        writer.add_scalar('Accuracy/val_epoch', val_acc, epoch)
+    writer.close()
+    logging.info('Training completed.')
+    logging.info(f'Best validation accuracy: {best_acc:.2f}%')
+    if args.evaluate:
+        evaluate(args, model, val_loader, None, device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return best_acc
+
+
+if __name__ == '__main__':
+    main()
