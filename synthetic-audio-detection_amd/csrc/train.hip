@@ -315,20 +315,42 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const T* __restrict__ x,
   }
 }
 
-// Forward finalize: batch mean / biased var (normalisation) and the running
-// stats update with the unbiased var (torch BatchNorm2d train mode).
-// stats = [mean | invstd | scale | shift], each [C].
-__global__ void bn_finalize_fwd_kernel(const float* __restrict__ part, int nb, int64_t P, int C,
-                                       const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                                       float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
-                                       float* __restrict__ stats) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nb; ++b) {
+// Sum of the nb per-workgroup partials of channel c (one 256-thread workgroup
+// per channel, float64 tree reduction).
+__device__ __forceinline__ void channel_partials(const float* __restrict__ part, int nb, int C, int c, double& s,
+                                                 double& q) {
+  __shared__ double red[2][4];
+  s = 0.0;
+  q = 0.0;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
     s += part[(int64_t)b * 2 * C + c];
     q += part[(int64_t)b * 2 * C + C + c];
   }
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    q += __shfl_xor(q, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s;
+    red[1][threadIdx.x >> 6] = q;
+  }
+  __syncthreads();
+  s = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  q = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+}
+
+// Forward finalize: batch mean / biased var (normalisation) and the running
+// stats update with the unbiased var (torch BatchNorm2d train mode).
+// stats = [mean | invstd | scale | shift], each [C].  Grid = C x 256 threads.
+__global__ __launch_bounds__(256) void bn_finalize_fwd_kernel(const float* __restrict__ part, int nb, int64_t P,
+                                                              int C, const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float eps,
+                                                              float momentum, float* __restrict__ rmean,
+                                                              float* __restrict__ rvar, float* __restrict__ stats) {
+  const int c = blockIdx.x;
+  double s, q;
+  channel_partials(part, nb, C, c, s, q);
+  if (threadIdx.x != 0) return;
   const double mean = s / (double)P;
   double var = q / (double)P - mean * mean;
   var = var < 0.0 ? 0.0 : var;
@@ -347,18 +369,16 @@ __global__ void bn_finalize_fwd_kernel(const float* __restrict__ part, int nb, i
 
 // Backward finalize: dbeta = sum dz, dgamma = sum dz*xhat (written, or added for
 // the never-zeroed layer3 grads of quirk C4); coef = [gamma*istd | sum dz / P |
-// sum dz*xhat / P].
-__global__ void bn_finalize_bwd_kernel(const float* __restrict__ part, int nb, int64_t P, int C,
-                                       const float* __restrict__ gamma, const float* __restrict__ stats,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta, int accumulate,
-                                       float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nb; ++b) {
-    s += part[(int64_t)b * 2 * C + c];
-    q += part[(int64_t)b * 2 * C + C + c];
-  }
+// sum dz*xhat / P].  Grid = C x 256 threads.
+__global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(const float* __restrict__ part, int nb, int64_t P,
+                                                              int C, const float* __restrict__ gamma,
+                                                              const float* __restrict__ stats,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                              int accumulate, float* __restrict__ coef) {
+  const int c = blockIdx.x;
+  double s, q;
+  channel_partials(part, nb, C, c, s, q);
+  if (threadIdx.x != 0) return;
   if (dgamma) dgamma[c] = (float)(accumulate ? (double)dgamma[c] + q : q);
   if (dbeta) dbeta[c] = (float)(accumulate ? (double)dbeta[c] + s : s);
   coef[c] = gamma[c] * stats[C + c];
@@ -604,10 +624,16 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g
   if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ void clip_coef_kernel(const double* __restrict__ part, int nb, float max_norm, float* __restrict__ out) {
-  if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(256) void clip_coef_kernel(const double* __restrict__ part, int nb, float max_norm,
+                                                        float* __restrict__ out) {
+  __shared__ double red[4];
   double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += part[b];
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) s += part[b];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  s = (red[0] + red[1]) + (red[2] + red[3]);
   const float norm = (float)sqrt(s);
   const float coef = max_norm / (norm + 1e-6f);
   out[0] = norm;
@@ -747,26 +773,27 @@ extern "C" int sad_stem_conv_run(const void* img, int64_t n, int32_t ih, int32_t
     SAD_CHECK_HIP(hipMalloc((void**)&zero_bias[dev], 512 * sizeof(float)));
     SAD_CHECK_HIP(hipMemset(zero_bias[dev], 0, 512 * sizeof(float)));
   }
-  ConvArgs a{};
-  a.in = col_ws;
-  a.in_pstride = 64;
+  SAD_REQUIRE(pix < (1ll << 31), "stem: too many pixels");
+  BlockConvArgs a{};
+  a.in0 = col_ws;
+  a.in0_pstride = 64;
   a.N = 1;
   a.H = 1;
   a.W = (int)pix;
   a.Cin = 64;
+  a.KH = a.KW = 1;
+  a.stride = 1;
+  a.pad = 0;
   a.wt = w_packed;
+  a.wt_ld = 64;
   a.bias = zero_bias[dev];
   a.out = out;
   a.out_pstride = 64;
   a.Ho = 1;
   a.Wo = (int)pix;
   a.Cout = 64;
-  a.KH = a.KW = 1;
-  a.stride = 1;
-  a.pad = 0;
   a.M = pix;
-  SAD_REQUIRE(pix < (1ll << 31), "stem: too many pixels");
-  return launch_conv(a, dtype, s);
+  return launch_block_conv(a, dtype, s);
 }
 
 static int bn_nblocks(int64_t P, int C) {
@@ -799,7 +826,7 @@ extern "C" int sad_bn_stats_run(const void* x, int64_t P, int32_t C, int32_t dty
     hipLaunchKernelGGL((bn_reduce_kernel<float, 0>), dim3(nb), dim3(256), 0, s, (const float*)x, P, C, nullptr,
                        nullptr, 1, nullptr, nullptr, nullptr, ws);
   SAD_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, nb, P, C, gamma, beta, eps,
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(C), dim3(256), 0, s, ws, nb, P, C, gamma, beta, eps,
                      momentum, running_mean, running_var, stats);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
@@ -867,7 +894,7 @@ extern "C" int sad_bn_backward_run(const void* x, int64_t P, int32_t C, int32_t 
     hipLaunchKernelGGL((bn_reduce_kernel<float, 1>), dim3(nb), dim3(256), 0, s, (const float*)x, P, C,
                        (const float*)dy, dpool, pool_hw > 0 ? pool_hw : 1, (const float*)y, stats, (float*)dz_out, ws);
   SAD_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, nb, P, C, gamma, stats,
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(C), dim3(256), 0, s, ws, nb, P, C, gamma, stats,
                      dgamma, dbeta, accumulate, coef);
   SAD_CHECK_HIP(hipGetLastError());
   const int64_t total = P * (C / 8);
@@ -944,7 +971,7 @@ extern "C" int sad_clip_grad_norm_run(float* g, int64_t n, float max_norm, float
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 4095) / 4096));
   hipLaunchKernelGGL(sqnorm_kernel, dim3(nb), dim3(256), 0, s, g, n, (double*)ws);
   SAD_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, s, (const double*)ws, nb, max_norm, norm_coef);
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, s, (const double*)ws, nb, max_norm, norm_coef);
   SAD_CHECK_HIP(hipGetLastError());
   if (n) {
     hipLaunchKernelGGL(scale_kernel, dim3(nblk(n)), dim3(256), 0, s, g, n, (const float*)norm_coef);

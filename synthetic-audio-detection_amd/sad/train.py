@@ -271,13 +271,20 @@ class TrainNet:
         return out
 
     def _conv(self, x, w, cout, k, stride, pad, res=None):
-        """raw NHWC conv (no BN) on the MFMA implicit-GEMM kernel; w packed [cout][k][k][cin]."""
+        """raw NHWC conv (no BN) on the MFMA block-conv kernels (the inference
+        backbone's); w packed [cout][k][k][cin].  ``res`` (added in the epilogue)
+        needs the bf16 halo kernel; fp32 with ``res`` runs the implicit-GEMM kernel."""
         N, H, W, Cin = x.shape
         Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
         out = torch.empty(N, Ho, Wo, cout, device=self.device, dtype=self.tdtype)
         with torch.cuda.device(self.device):
-            _lib.call('sad_conv2d_run', _lib.ptr(x), N, H, W, Cin, _lib.ptr(w), _lib.ptr(self.zero_bias),
-                      _lib.ptr(res), _lib.ptr(out), cout, k, stride, pad, 0, self._dt, 0, self._stream())
+            if res is not None and self._dt != _lib.SAD_BF16:
+                _lib.call('sad_conv2d_run', _lib.ptr(x), N, H, W, Cin, _lib.ptr(w), _lib.ptr(self.zero_bias),
+                          _lib.ptr(res), _lib.ptr(out), cout, k, stride, pad, 0, self._dt, 0, self._stream())
+            else:
+                _lib.call('sad_block_conv_run', _lib.ptr(x), N, H, W, Cin, None, 0, 0, 0, 1, _lib.ptr(w), 0,
+                          _lib.ptr(self.zero_bias), _lib.ptr(res), _lib.ptr(out), cout, k, stride, pad, 0, self._dt,
+                          0, self._stream())
         return out
 
     def _bn_backward(self, x, st, key, grads, dy=None, dpool=None, pool_hw=0, y=None, accumulate=False,
@@ -514,10 +521,10 @@ class Trainer:
         if self.world > 1:
             import torch.distributed as dist
             dist.all_reduce(lc, group=self.group)
-        loss_sum, correct = lc.tolist()
-        loss = loss_sum / global_batch
-        if not math.isfinite(loss):  # NaN/Inf: skip the step (:266-271)
-            return loss, 0, 0, False
+        # The backward and the gradient all-reduce are queued BEFORE the host
+        # reads the loss, so the device never idles on that sync; a NaN/Inf loss
+        # (:266-271) then discards them (layer4 grads are overwritten by the next
+        # backward, the layer3 step gradient is simply not folded in).
         net.backward(dfeat, saved, layers, self.grads3)
         a4, b4 = net.range4
         if self.world > 1:
@@ -525,6 +532,10 @@ class Trainer:
             dist.all_reduce(net.gflat[a4:b4], group=self.group)
             if self.layer3_unfrozen:
                 dist.all_reduce(self._g3flat, group=self.group)
+        loss_sum, correct = lc.tolist()
+        loss = loss_sum / global_batch
+        if not math.isfinite(loss):  # skip the step
+            return loss, 0, 0, False
         lo = a4
         if self.layer3_unfrozen:
             a3, b3 = net.range3
