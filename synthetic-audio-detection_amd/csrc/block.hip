@@ -176,24 +176,60 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
     __builtin_amdgcn_sched_barrier(0);
     if (g + S - 1 < total && !(a.ablate & 1)) issue(S == 3 ? (st == 0 ? 2 : st - 1) : (st ^ 1));
     const char* base = smem + st * STAGE;
+    if constexpr (TC * TP > 16) {
+      // 128x64 wave tiles: 128 accumulator VGPRs leave room for one K-half's
+      // fragments only (two waves per SIMD)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        uint4 wf[TC], pf[TP];
+        const int c = fg + 4 * s;
+#pragma unroll
+        for (int i = 0; i < TC; ++i) {
+          const int r = BP + wc * 16 * TC + i * 16 + fr;
+          wf[i] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < TP; ++j) {
+          const int r = wp * 16 * TP + j * 16 + fr;
+          pf[j] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TC; ++i)
+#pragma unroll
+          for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pf[j], acc[i][j]);
+      }
+    } else {
+    // both K-halves' fragments in registers; half 1's reads are issued between
+    // half 0's MFMAs (sched_group_barrier), so only half 0's read latency is
+    // exposed per K-step (the co-resident wave covers it)
+    uint4 wf[2][TC], pf[2][TP];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      uint4 wf[TC], pf[TP];
       const int c = fg + 4 * s;
 #pragma unroll
       for (int i = 0; i < TC; ++i) {
         const int r = BP + wc * 16 * TC + i * 16 + fr;
-        wf[i] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
+        wf[s][i] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
       }
 #pragma unroll
       for (int j = 0; j < TP; ++j) {
         const int r = wp * 16 * TP + j * 16 + fr;
-        pf[j] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
+        pf[s][j] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
       }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < TC; ++i)
 #pragma unroll
-        for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pf[j], acc[i][j]);
+        for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[s][i], pf[s][j], acc[i][j]);
+    __builtin_amdgcn_sched_group_barrier(0x100, TC + TP, 0);
+#pragma unroll
+    for (int k = 0; k < TC + TP; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * TC * TP - (TC + TP), 0);
     }
     st = st + 1 == S ? 0 : st + 1;
     if (++cks == nk) {
