@@ -33,6 +33,7 @@ struct FrontendPlan {
   sad_frontend_cfg cfg;
   int n_frames;
   int bin_lo, bin_hi;         // mel bank nonzero bin range [lo, hi]
+  int nnz = 0;                // packed mel weights
   float2* d_tw1024 = nullptr;  // e^{-2 pi i m / 1024}, m < 1024
   float2* d_tw2048 = nullptr;  // e^{-2 pi i k / 2048}, k <= 1024
   float* d_window = nullptr;   // periodic Hann(2048)
@@ -47,24 +48,53 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+// LDS exchange between the lanes of ONE wave: the wave's LDS operations
+// complete in order, so a compiler fence at wavefront scope is all that is
+// needed (no workgroup barrier: the four waves run independent frames).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int FE_STAGE_MELS = 128;  // dB rows staged in LDS for coalesced stores
+constexpr int FE_POW = FE_NC + 4;   // power bins per wave in LDS (any bin range of the 1025)
+constexpr int FE_MAX_NNZ = 1600;    // mel weights in LDS (1515 for the reference's bank)
+// LDS: twiddles 8 KB + 4 FFT buffers 32 KB + power 16 KB + dB staging 16.5 KB +
+// mel weights 6.3 KB = 79 KB: two workgroups per CU.
+
 template <typename IT>  // int16_t PCM (scaled by 1/32768, torchaudio.load normalize) or float
-__global__ __launch_bounds__(256) void fe_mel_db_kernel(
+__global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     const IT* __restrict__ pcm, int64_t seg_stride, int n_samples, int n_frames, int hop,
-    const float2* __restrict__ tw1024, const float2* __restrict__ tw2048,
-    const float* __restrict__ window, const int* __restrict__ mel_start,
-    const int* __restrict__ mel_len, const int* __restrict__ mel_off,
-    const float* __restrict__ mel_w, int n_mels, int bin_lo, int bin_hi, float* __restrict__ out) {
+    const float2* __restrict__ tw1024, const float* __restrict__ window, const int* __restrict__ mel_start,
+    const int* __restrict__ mel_len, const int* __restrict__ mel_off, const float* __restrict__ mel_w, int nnz,
+    int n_mels, int bin_lo, int bin_hi, float* __restrict__ out) {
   __shared__ float2 s_tw[FE_NC];
-  __shared__ float2 s_tw2[FE_NC + 1];
   __shared__ float2 s_buf[FE_WAVES][FE_NC];
-  __shared__ float s_pow[FE_WAVES][FE_NC];
+  __shared__ float s_pow[FE_WAVES][FE_POW];
+  __shared__ float s_db[FE_STAGE_MELS][FE_FRAMES_PER_WG + 1];
+  __shared__ float s_melw[FE_MAX_NNZ];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t seg = blockIdx.y;
   const IT* x = pcm + seg * seg_stride;
   const float in_scale = sizeof(IT) == 2 ? (1.0f / 32768.0f) : 1.0f;
+  const bool staged = n_mels <= FE_STAGE_MELS && bin_hi - bin_lo < FE_POW && nnz <= FE_MAX_NNZ;
   for (int i = tid; i < FE_NC; i += 256) s_tw[i] = tw1024[i];
-  for (int i = tid; i <= FE_NC; i += 256) s_tw2[i] = tw2048[i];
+  if (staged)
+    for (int i = tid; i < nnz; i += 256) s_melw[i] = mel_w[i];
+  // this lane's mel rows (staged path): m = lane and n_mels-1-lane -- filters
+  // widen with m, so the pair's lengths sum to about the same for every lane
+  int mm[2], mk0[2], mlen[2], moff[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int m = q == 0 ? lane : n_mels - 1 - lane;
+    const bool ok = q == 0 ? lane < n_mels : m >= 64;
+    mm[q] = ok ? m : -1;
+    mk0[q] = ok ? mel_start[m] : 0;
+    mlen[q] = ok ? mel_len[m] : 0;
+    moff[q] = ok ? mel_off[m] : 0;
+  }
   __syncthreads();
 
   const int f_begin = blockIdx.x * FE_FRAMES_PER_WG;
@@ -72,97 +102,128 @@ __global__ __launch_bounds__(256) void fe_mel_db_kernel(
   float2* buf = s_buf[wave];
   float* pw = s_pow[wave];
   const int pad = FE_NFFT / 2;
+  // aligned pair loads need an even sample offset for every frame and pair
+  const bool pairs = ((hop & 1) == 0) && ((seg_stride & 1) == 0) && ((((uintptr_t)pcm) & (2 * sizeof(IT) - 1)) == 0);
 
-  for (int f0 = f_begin; f0 < f_end; f0 += FE_WAVES) {
-    const int t = f0 + wave;
-    const bool active = t < f_end;  // wave-uniform
+  for (int t = f_begin + wave; t < f_end; t += FE_WAVES) {
     float2 v[4][4];
-    // ---- pass 0 (Ns = 1): load z[j + 256 r] straight from global
-    if (active) {
+    // ---- pass 0 input: z[m] = (y[2m], y[2m+1]) windowed, m = j + 256 r; one
+    // 2-sample load per lane (coalesced) where the frame needs no reflection
+    const int base = t * hop - pad;
+    const bool inside = pairs && base >= 0 && base + FE_NFFT <= n_samples;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int j = lane + 64 * b;
+    for (int b = 0; b < 4; ++b) {
+      const int j = lane + 64 * b;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = j + 256 * r;
-          float e[2];
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int n = 2 * m + q;
-            int idx = t * hop + n - pad;
-            idx = idx < 0 ? -idx : idx;
-            idx = idx >= n_samples ? 2 * (n_samples - 1) - idx : idx;
-            e[q] = (float)x[idx] * in_scale * window[n];
+      for (int r = 0; r < 4; ++r) {
+        const int m = j + 256 * r;
+        float e0, e1;
+        if (inside) {
+          if constexpr (sizeof(IT) == 2) {
+            const uint32_t u = *(const uint32_t*)(x + base + 2 * m);
+            e0 = (float)(short)(u & 0xFFFF);
+            e1 = (float)(short)(u >> 16);
+          } else {
+            const float2 f = *(const float2*)(x + base + 2 * m);
+            e0 = f.x;
+            e1 = f.y;
           }
-          v[b][r] = make_float2(e[0], e[1]);
+        } else {
+          int i0 = base + 2 * m, i1 = i0 + 1;
+          i0 = i0 < 0 ? -i0 : i0;
+          i0 = i0 >= n_samples ? 2 * (n_samples - 1) - i0 : i0;
+          i1 = i1 < 0 ? -i1 : i1;
+          i1 = i1 >= n_samples ? 2 * (n_samples - 1) - i1 : i1;
+          e0 = (float)x[i0];
+          e1 = (float)x[i1];
         }
+        const float2 wv = *(const float2*)(window + 2 * m);
+        v[b][r] = make_float2(e0 * in_scale * wv.x, e1 * in_scale * wv.y);
       }
     }
-    // ---- 5 radix-4 Stockham passes, Ns = 1, 4, 16, 64, 256
+    // ---- 5 radix-4 Stockham passes, Ns = 1, 4, 16, 64, 256 (wave-local)
 #pragma unroll
     for (int p = 0; p < 5; ++p) {
       const int Ns = 1 << (2 * p);
-      if (active) {
-        if (p > 0) {
-#pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const int j = lane + 64 * b;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[b][r] = buf[j + 256 * r];
-          }
-        }
-      }
-      __syncthreads();
-      if (active) {
+      if (p > 0) {
+        wave_lds_sync();
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int j = lane + 64 * b;
-          const int k = j & (Ns - 1);
-          if (p > 0) {
-            const int tstep = FE_NC / (Ns * 4);  // angle index step per r
 #pragma unroll
-            for (int r = 1; r < 4; ++r) v[b][r] = cmul(v[b][r], s_tw[(k * r * tstep) & (FE_NC - 1)]);
-          }
-          // radix-4 forward DFT
-          const float2 a0 = v[b][0], a1 = v[b][1], a2 = v[b][2], a3 = v[b][3];
-          const float2 s02 = make_float2(a0.x + a2.x, a0.y + a2.y);
-          const float2 d02 = make_float2(a0.x - a2.x, a0.y - a2.y);
-          const float2 s13 = make_float2(a1.x + a3.x, a1.y + a3.y);
-          const float2 d13 = make_float2(a1.x - a3.x, a1.y - a3.y);
-          const int idxD = (j / Ns) * Ns * 4 + k;
-          buf[idxD] = make_float2(s02.x + s13.x, s02.y + s13.y);
-          buf[idxD + Ns] = make_float2(d02.x + d13.y, d02.y - d13.x);      // a0 - i a1 - a2 + i a3
-          buf[idxD + 2 * Ns] = make_float2(s02.x - s13.x, s02.y - s13.y);
-          buf[idxD + 3 * Ns] = make_float2(d02.x - d13.y, d02.y + d13.x);  // a0 + i a1 - a2 - i a3
+          for (int r = 0; r < 4; ++r) v[b][r] = buf[j + 256 * r];
+        }
+        wave_lds_sync();
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int j = lane + 64 * b;
+        const int k = j & (Ns - 1);
+        if (p > 0) {
+          const int tstep = FE_NC / (Ns * 4);  // angle index step per r
+#pragma unroll
+          for (int r = 1; r < 4; ++r) v[b][r] = cmul(v[b][r], s_tw[(k * r * tstep) & (FE_NC - 1)]);
+        }
+        // radix-4 forward DFT
+        const float2 a0 = v[b][0], a1 = v[b][1], a2 = v[b][2], a3 = v[b][3];
+        const float2 s02 = make_float2(a0.x + a2.x, a0.y + a2.y);
+        const float2 d02 = make_float2(a0.x - a2.x, a0.y - a2.y);
+        const float2 s13 = make_float2(a1.x + a3.x, a1.y + a3.y);
+        const float2 d13 = make_float2(a1.x - a3.x, a1.y - a3.y);
+        const int idxD = (j / Ns) * Ns * 4 + k;
+        buf[idxD] = make_float2(s02.x + s13.x, s02.y + s13.y);
+        buf[idxD + Ns] = make_float2(d02.x + d13.y, d02.y - d13.x);      // a0 - i a1 - a2 + i a3
+        buf[idxD + 2 * Ns] = make_float2(s02.x - s13.x, s02.y - s13.y);
+        buf[idxD + 3 * Ns] = make_float2(d02.x - d13.y, d02.y + d13.x);  // a0 + i a1 - a2 - i a3
+      }
+    }
+    wave_lds_sync();
+    // ---- real-spectrum recovery + power for bins [bin_lo, bin_hi]
+    for (int k = bin_lo + lane; k <= bin_hi; k += 64) {
+      const float2 A = buf[k & (FE_NC - 1)];
+      const float2 Bc = buf[(FE_NC - k) & (FE_NC - 1)];
+      const float2 B = make_float2(Bc.x, -Bc.y);              // conj(Z[N/2-k])
+      const float2 E = make_float2(0.5f * (A.x + B.x), 0.5f * (A.y + B.y));
+      const float2 D = make_float2(A.x - B.x, A.y - B.y);
+      const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);  // -i/2 (A - B)
+      // e^{-2 pi i k / 2048}: the 1024-point table at k/2, times e^{-2 pi i / 2048} for odd k
+      float2 w2 = s_tw[(k >> 1) & (FE_NC - 1)];
+      if (k == FE_NC) w2 = make_float2(-1.f, 0.f);
+      if (k & 1) w2 = cmul(w2, make_float2(0.99999529380957619f, -0.0030679567629659761f));
+      const float2 WO = cmul(w2, O);
+      const float re = E.x + WO.x, im = E.y + WO.y;
+      pw[k - bin_lo] = re * re + im * im;
+    }
+    wave_lds_sync();
+    if (staged) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (mm[q] >= 0) {
+          const float* pp = pw + mk0[q] - bin_lo;
+          const float* ww = s_melw + moff[q];
+          float acc = 0.f;
+          for (int i = 0; i < mlen[q]; ++i) acc = fmaf(pp[i], ww[i], acc);
+          s_db[mm[q]][t - f_begin] = 10.0f * log10f(fmaxf(acc, 1e-10f));
         }
       }
-      __syncthreads();
-    }
-    // ---- real-spectrum recovery + power for bins [bin_lo, bin_hi]
-    if (active) {
-      for (int k = bin_lo + lane; k <= bin_hi; k += 64) {
-        const float2 A = buf[k & (FE_NC - 1)];
-        const float2 Bc = buf[(FE_NC - k) & (FE_NC - 1)];
-        const float2 B = make_float2(Bc.x, -Bc.y);              // conj(Z[N/2-k])
-        const float2 E = make_float2(0.5f * (A.x + B.x), 0.5f * (A.y + B.y));
-        const float2 D = make_float2(A.x - B.x, A.y - B.y);
-        const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);  // -i/2 (A - B)
-        const float2 WO = cmul(s_tw2[k], O);
-        const float re = E.x + WO.x, im = E.y + WO.y;
-        pw[k - bin_lo] = re * re + im * im;
-      }
-    }
-    __syncthreads();
-    if (active) {
+    } else {
       for (int m = lane; m < n_mels; m += 64) {
         const int k0 = mel_start[m], len = mel_len[m], off = mel_off[m];
         float acc = 0.f;
         for (int q = 0; q < len; ++q) acc = fmaf(pw[k0 + q - bin_lo], mel_w[off + q], acc);
-        const float db = 10.0f * log10f(fmaxf(acc, 1e-10f));
-        out[(seg * n_mels + m) * n_frames + t] = db;
+        out[(seg * n_mels + m) * n_frames + t] = 10.0f * log10f(fmaxf(acc, 1e-10f));
       }
     }
+    wave_lds_sync();  // pw / buf are rewritten by the next frame
+  }
+  if (staged) {
+    // [n_mels][frames of this block] -> rows of up to 32 consecutive frames
     __syncthreads();
+    const int nf = f_end - f_begin;
+    for (int i = tid; i < n_mels * FE_FRAMES_PER_WG; i += 256) {
+      const int m = i / FE_FRAMES_PER_WG, f = i - m * FE_FRAMES_PER_WG;
+      if (f < nf) out[(seg * n_mels + m) * n_frames + f_begin + f] = s_db[m][f];
+    }
   }
 }
 
@@ -300,6 +361,7 @@ extern "C" int sad_frontend_plan_create(const sad_frontend_cfg* cfg, sad_fronten
   }
   p->bin_lo = lo;
   p->bin_hi = hi;
+  p->nnz = (int)w.size();
   std::vector<float2> tw(FE_NC), tw2(FE_NC + 1);
   for (int m = 0; m < FE_NC; ++m) {
     const double a = -2.0 * M_PI * m / FE_NC;
@@ -363,9 +425,8 @@ static int frontend_run(const sad_frontend_plan* p, const IT* pcm, int64_t n_seg
     const size_t off = (size_t)done * p->cfg.n_mels * p->n_frames;
     hipLaunchKernelGGL(fe_mel_db_kernel<IT>, dim3(n_fb, (unsigned)chunk), dim3(256), 0, s,
                        pcm + done * seg_stride, seg_stride, p->cfg.n_samples, p->n_frames,
-                       p->cfg.hop_length, p->d_tw1024, p->d_tw2048, p->d_window, p->d_mel_start,
-                       p->d_mel_len, p->d_mel_off, p->d_mel_w, p->cfg.n_mels, p->bin_lo, p->bin_hi,
-                       dbbuf + off);
+                       p->cfg.hop_length, p->d_tw1024, p->d_window, p->d_mel_start, p->d_mel_len,
+                       p->d_mel_off, p->d_mel_w, p->nnz, p->cfg.n_mels, p->bin_lo, p->bin_hi, dbbuf + off);
     SAD_CHECK_HIP(hipGetLastError());
     hipLaunchKernelGGL(fe_normalize_kernel, dim3((unsigned)chunk), dim3(1024), 0, s, dbbuf + off,
                        p->cfg.n_mels * p->n_frames, p->cfg.top_db, out_map + off);
