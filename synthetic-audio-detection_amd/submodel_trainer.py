@@ -252,7 +252,8 @@ def _allreduce_sum(values, model):
     if model.world <= 1:
         return values
     import torch.distributed as dist
-    t = torch.tensor(values, dtype=torch.float64, device=model.trainer.device)
+    dev = 'cpu' if dist.get_backend(model.group) == 'gloo' else model.trainer.device
+    t = torch.tensor(values, dtype=torch.float64, device=dev)
     dist.all_reduce(t, group=model.group)
     return t.tolist()
 
@@ -322,14 +323,20 @@ def _eval_pass(val_loader, model):
         preds.extend(pred.cpu().numpy().tolist())
         tgts.extend(targets.numpy().tolist())
     loss_sum, correct, total = _allreduce_sum([loss_sum, correct, total], model)
-    if model.world > 1:
-        import torch.distributed as dist
-        gp, gt = [None] * model.world, [None] * model.world
-        dist.all_gather_object(gp, preds, group=model.group)
-        dist.all_gather_object(gt, tgts, group=model.group)
-        preds = [p for r in gp for p in r]
-        tgts = [t for r in gt for t in r]
+    preds, tgts = _gather_lists(preds, tgts, model)
     return loss_sum, int(correct), int(total), preds, tgts
+
+
+def _gather_lists(preds, tgts, model):
+    """Every rank's predictions / targets, in rank order (the reference's DP
+    evaluates the whole validation set in one process, :354-355)."""
+    if model.world <= 1:
+        return preds, tgts
+    import torch.distributed as dist
+    gp, gt = [None] * model.world, [None] * model.world
+    dist.all_gather_object(gp, preds, group=model.group)
+    dist.all_gather_object(gt, tgts, group=model.group)
+    return [p for r in gp for p in r], [t for r in gt for t in r]
 
 
 def validate(args, val_loader, model, criterion, epoch, device):

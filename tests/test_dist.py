@@ -61,3 +61,35 @@ def test_gather_rows_world2_ragged():
 
 def test_gather_rows_world3():
     _run(3, 10)
+
+
+def _trainer_worker(rank, world, port, q):
+    """submodel_trainer's cross-rank reductions (validation totals, prediction
+    gathering) on a gloo group: rank r contributes loss r+1, r correct of r+2."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import submodel_trainer as smt
+
+    class _T:
+        device = 'cpu'
+    model = smt.DeviceModel(_T(), None, rank, world, dist.group.WORLD)
+    tot = smt._allreduce_sum([float(rank + 1), float(rank), float(rank + 2)], model)
+    preds, tgts = smt._gather_lists([rank] * (rank + 1), [10 + rank] * (rank + 1), model)
+    q.put((rank, tot, preds, tgts))
+    dist.destroy_process_group()
+
+
+def test_trainer_reductions_world2():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_trainer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, tot, preds, tgts in res:
+        assert tot == [3.0, 1.0, 5.0]
+        assert preds == [0, 1, 1] and tgts == [10, 11, 11]
