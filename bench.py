@@ -8,10 +8,12 @@ counter-hash PRNG, rank-disjoint ranges) -> fused STFT/mel/dB/standardise ->
 fused resize+stem -> ResNet-18 (bf16 MFMA implicit GEMM) -> 6 heads + merge ->
 RCCL all-gather of the merged logits to every rank (N > 1).  Weak scaling.
 
-Prints ONE JSON line on rank 0 (driver contract) with `roofline` (the backbone
-conv kernels, MFMA-bound, timed with HIP events on their stream inside the timed
-region) and `cpu_baseline` (the CPU oracle in the reference's structure, on a
-bounded sample, rank 0 at N=1 only).
+Prints ONE JSON line on rank 0 (driver contract) with `roofline` (the dominant
+kernel, the 256x256 block-conv of layer3/4, MFMA-bound: algorithmic FLOPs of its
+launches in the last timed step over their HIP-event durations recorded by
+libsad on the launch stream; `traffic` from the committed PMC passes; the whole
+backbone's rate as `roofline.backbone`) and `cpu_baseline` (the CPU oracle in the
+reference's structure, on a bounded sample, rank 0 at N=1 only).
 """
 import argparse
 import json
@@ -31,6 +33,11 @@ SEG = 128000
 BACKBONE_FLOP = 18.13e9        # ResNet-18 @512^2 with conv1's 3 identical channels folded (reference: 18.95e9)
 REF_BACKBONE_FLOP = 18.95e9
 BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+# The dominant kernel (33% of the step, profiles/r01_bench_kernels_44k.md) and its
+# rocprof key in profiles/r01_pmc_traffic.json; 1344 TFLOP/s = the best bf16 GEMM
+# measured on this box (tools/gemm_ref.py)
+DOMINANT_VARIANT = 13
+DOMINANT_KERNEL = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1>|131072'
 F32_PEAK_TFLOPS = 157.3
 
 
@@ -115,13 +122,20 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if i == args.steps - 1:
+            # HIP events around each block-conv launch of the last timed step, on
+            # its stream (events between launches cost the step ~5%, so one step only)
+            _lib.call('sad_profile_begin')
         step(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    k_ms, k_n, k_fl = _lib.ctypes.c_double(), _lib.I64(), _lib.ctypes.c_double()
+    _lib.call('sad_profile_end', DOMINANT_VARIANT, _lib.ctypes.byref(k_ms), _lib.ctypes.byref(k_n),
+              _lib.ctypes.byref(k_fl))
     bb_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
@@ -132,6 +146,15 @@ def main():
     if rank == 0:
         peak = BF16_PEAK_TFLOPS if args.dtype == 'bf16' else F32_PEAK_TFLOPS
         achieved = BACKBONE_FLOP * B / (bb_ms * 1e-3) / 1e12
+        n_l = max(k_n.value, 1)
+        k_avg_us = k_ms.value * 1e3 / n_l
+        k_tf = k_fl.value / (k_ms.value * 1e-3) / 1e12 if k_ms.value > 0 else 0.0
+        traffic = None
+        tj = os.path.join(ROOT, 'profiles', 'r01_pmc_traffic.json')
+        if os.path.exists(tj) and args.dtype == 'bf16':
+            rec = json.load(open(tj)).get(DOMINANT_KERNEL)
+            if rec and rec.get('hbm_read_bytes') is not None:
+                traffic = rec['hbm_read_bytes'] + rec['hbm_write_bytes']
         out = {
             'metric': '4s@32kHz segments/sec end-to-end (mel+ResNet+ensemble), 1/2/4/8 MI355X',
             'value': round(value, 1), 'unit': 'segments/s', 'n_gpus': world, 'steps': args.steps,
@@ -143,11 +166,19 @@ def main():
                                    '-> ResNet-18@512x512 -> 6 binary heads -> merge (+RCCL all-gather of logits)',
                        'segments_per_gpu_per_step': B, 'heads': args.heads, 'distinct_backbones': 1,
                        'micro_batch': args.micro_batch, 'parallelism': f'dp{world}'},
-            'roofline': {'bound': 'mfma', 'kernel': 'backbone: fused resize+stem + 19 implicit-GEMM convs + avgpool',
-                         'achieved': round(achieved, 1), 'peak': peak, 'unit': 'TFLOP/s',
-                         'frac': round(achieved / peak, 4), 'traffic': None,
-                         'backbone_ms_per_step': round(bb_ms, 3),
-                         'flop_per_segment': BACKBONE_FLOP},
+            'roofline': {'bound': 'mfma',
+                         'kernel': 'sad::block_conv_kernel 256x256 tile (variant 13): the layer3 + layer4 convs, '
+                                   '8 launches per micro-batch, 33% of the step',
+                         'achieved': round(k_tf, 1), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(k_tf / peak, 4),
+                         'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, '
+                                                             'profiles/r01_pmc_traffic.json)',
+                         'launches': k_n.value, 'launch_avg_us': round(k_avg_us, 2),
+                         'flop_per_launch': round(k_fl.value / n_l),
+                         'backbone': {'achieved': round(achieved, 1), 'frac': round(achieved / peak, 4),
+                                      'ms_per_step': round(bb_ms, 3), 'flop_per_segment': BACKBONE_FLOP,
+                                      'what': 'fused resize+stem + 16 block-conv GEMMs + avgpool, HIP events '
+                                              'around the backbone call'},
+                         'measured_gemm_ceiling_tflops': 1344.0},
         }
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline()

@@ -134,6 +134,16 @@ int sad_backbone_run_debug(const sad_backbone_plan* plan, const float* map, int6
                            float* feats, void* layer4_out, void* workspace, size_t ws_bytes,
                            void* stream);
 
+/* Kernel-level timing of the backbone's block-conv launches (bench.py's
+ * roofline of the dominant kernel): between begin and end, every block-conv
+ * launch of sad_backbone_run* is bracketed by HIP events on its stream.  end()
+ * synchronises those events and returns, for the launches of tile `variant`
+ * (0 = all), the summed kernel time, the launch count and their algorithmic
+ * FLOPs (2*M*Cout*K with K the conv taps [+ the downsample], never the
+ * identity shortcut's columns). */
+int sad_profile_begin(void);
+int sad_profile_end(int32_t variant, double* total_ms, int64_t* launches, double* flops);
+
 /* ------------------------------------------------------------------ heads */
 /* Replaces BinaryClassifier.head (inference_runner.py:36-48) for N sub-models
  * and ModularMultiHeadClassifier.forward (inference_runner.py:62-73).

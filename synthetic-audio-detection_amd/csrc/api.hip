@@ -4,6 +4,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -258,6 +259,67 @@ extern "C" int sad_backbone_workspace_size(const sad_backbone_plan* p, int64_t m
   return SAD_OK;
 }
 
+// ---- launch timing of the block-conv kernels (sad_profile_*): HIP events on
+// the launch stream around each launch, keyed by tile variant, with the
+// launch's algorithmic FLOPs (the identity shortcut's K columns excluded).
+struct ProfRec {
+  int variant;
+  double flops;
+  hipEvent_t e0, e1;
+};
+static std::mutex g_prof_mu;
+static bool g_prof_on = false;
+static std::vector<ProfRec> g_prof;
+
+static int timed_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, double flops) {
+  if (!g_prof_on) return launch_block_conv(a, dtype, s);
+  ProfRec r{default_block_variant(a, dtype), flops, nullptr, nullptr};
+  SAD_CHECK_HIP(hipEventCreate(&r.e0));
+  SAD_CHECK_HIP(hipEventCreate(&r.e1));
+  SAD_CHECK_HIP(hipEventRecord(r.e0, s));
+  int rc = launch_block_conv(a, dtype, s);
+  SAD_CHECK_HIP(hipEventRecord(r.e1, s));
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof.push_back(r);
+  return rc;
+}
+
+extern "C" int sad_profile_begin(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto& r : g_prof) {
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+  }
+  g_prof.clear();
+  g_prof_on = true;
+  return SAD_OK;
+}
+
+extern "C" int sad_profile_end(int32_t variant, double* total_ms, int64_t* launches, double* flops) {
+  SAD_REQUIRE(total_ms && launches && flops, "null outputs");
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_on = false;
+  double ms = 0.0, fl = 0.0;
+  int64_t n = 0;
+  for (auto& r : g_prof) {
+    if (variant == 0 || r.variant == variant) {
+      SAD_CHECK_HIP(hipEventSynchronize(r.e1));
+      float t = 0.f;
+      SAD_CHECK_HIP(hipEventElapsedTime(&t, r.e0, r.e1));
+      ms += t;
+      fl += r.flops;
+      ++n;
+    }
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+  }
+  g_prof.clear();
+  *total_ms = ms;
+  *launches = n;
+  *flops = fl;
+  return SAD_OK;
+}
+
 // Blocks [b0, b1) of the block path on n segments: *in (NHWC, H x H x C) ->
 // *in (the last output; the buffers *in, *alt, tmp rotate).
 static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t n, void** in, void** alt, void* tmp,
@@ -288,7 +350,7 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
       a.Cout = blk.cout;
       a.relu = 1;
       a.M = mb * Ho * Ho;
-      if ((rc = launch_block_conv(a, p->dtype, s))) return rc;
+      if ((rc = timed_block_conv(a, p->dtype, s, 2.0 * a.M * a.Cout * 9.0 * C))) return rc;
       BlockConvArgs b2 = a;
       b2.in0 = bufT;
       b2.in0_pstride = blk.cout;
@@ -310,7 +372,9 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
       b2.wt = blk.w2;
       b2.bias = blk.b2;
       b2.out = bufB;
-      if ((rc = launch_block_conv(b2, p->dtype, s))) return rc;
+      // algorithmic work: conv2, plus the 1x1 downsample when there is one (not the identity)
+      const double fl2 = 2.0 * b2.M * b2.Cout * (9.0 * blk.cout + (blk.stride != 1 ? (double)C : 0.0));
+      if ((rc = timed_block_conv(b2, p->dtype, s, fl2))) return rc;
       std::swap(bufA, bufB);
       H = Ho;
       C = blk.cout;

@@ -17,6 +17,6 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-forma
 T=$(find $OUT/trace -name 'run_kernel_trace.csv' | head -1 | xargs dirname)
 F=$(find $OUT/fetch -name 'run_counter_collection.csv' | head -1 | xargs dirname)
 W=$(find $OUT/write -name 'run_counter_collection.csv' | head -1 | xargs dirname)
-python3 tools/profsum.py --trace $T --fetch $F --write $W --steps 4 > $OUT.md
+python3 tools/profsum.py --trace $T --fetch $F --write $W --steps 4 --json $OUT.traffic.json > $OUT.md
 tail -1 $OUT/trace.log >> $OUT.md
 cp $(find $OUT/trace -name 'run_kernel_stats.csv' | head -1) $OUT.stats.csv

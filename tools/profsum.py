@@ -43,11 +43,22 @@ def main():
     ap.add_argument('--fetch')
     ap.add_argument('--write')
     ap.add_argument('--steps', type=int, required=True, help='steps in the traced run (warmup + timed)')
+    ap.add_argument('--json', help='also write {kernel: {avg_us, hbm_read_bytes, hbm_write_bytes}} here '
+                                   '(bench.py reads it for roofline.traffic)')
     a = ap.parse_args()
     tr = load_trace(a.trace)
     fe = load_pmc(a.fetch, 'FETCH_SIZE')
     wr = load_pmc(a.write, 'WRITE_SIZE')
     tot = sum(v[1] for v in tr.values()) / a.steps
+    if a.json:
+        import json
+        out = {}
+        for k, (n, t) in tr.items():
+            f, w = fe.get(k), wr.get(k)
+            out[f'{k[0]}|{k[1]}'] = {'avg_us': t / n / 1e3, 'launches_per_step': n / a.steps,
+                                     'hbm_read_bytes': None if f is None else 2 * f * 1024,
+                                     'hbm_write_bytes': None if w is None else w * 1024}
+        json.dump(out, open(a.json, 'w'), indent=1)
     print('| kernel | grid (threads) | launches/step | avg us | ms/step | share | HBM read MB/launch (2xFETCH) | HBM write MB/launch |')
     print('|---|---|---|---|---|---|---|---|')
     for k, (n, t) in sorted(tr.items(), key=lambda x: -x[1][1]):
