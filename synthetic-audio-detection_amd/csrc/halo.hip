@@ -75,12 +75,16 @@ struct HaloGeo {
   static constexpr int RES = BP * 128;
   static constexpr int WST = BC * 128;
   static constexpr int NWS = 5;                 // weight ring stages (NWS-1 steps ahead)
+  // patch pieces of the next chunk go out over taps [0, PT) (<= 3 per wave and
+  // step), the tile's residual rows over taps [2, 2 + RT)
+  static constexpr int PT = QP <= 12 ? 4 : 7;
+  static constexpr int RT = 4;
   static constexpr int OFF_RES = 2 * PATCH, OFF_W = 2 * PATCH + RES;
   static constexpr int SMEM = OFF_W + NWS * WST;
   static_assert(TW == 16, "a 16-pixel fragment is one tile row");
   static_assert(BP % TW == 0 && NW % 2 == 0, "tile shape");
   static_assert(NDR % NL == 0 && BC % (8 * NL) == 0, "DMA split");
-  static_assert(QP <= 12, "patch pieces must fit taps 0-3 at 3 per step");
+  static_assert(QP <= 3 * PT && PT <= 8, "patch pieces must be issued before the next chunk's last tap");
 };
 
 template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU>
@@ -164,7 +168,7 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
       const int oy0 = (rem / tiles_x) * TH, ox0 = (rem % tiles_x) * TW;
 #pragma unroll
       for (int k = 0; k < QR; ++k) {
-        if (k % 4 != tap - 2) continue;
+        if (k % G::RT != tap - 2) continue;
         const int q = lw + NL * k;
         const int p = 8 * q + (lane >> 3);
         const int ty = p / TW, tx = p - ty * TW;
@@ -317,16 +321,16 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
         if (wloader) {
           if (!(ab & 16)) load_weights();
         } else if (!(ab & 32)) {
-          if constexpr (tap < 4) {
+          if constexpr (tap < G::PT) {
 #pragma unroll
-            for (int k = tap; k < QP; k += 4)
+            for (int k = tap; k < QP; k += G::PT)
               if (NDP % NL == 0 || lw + NL * k < NDP)
                 dma16_m0(r0, poff[k], lds0 + (pbuf ^ 1) * G::PATCH + (lw + NL * k) * 1024);
-            if constexpr (tap == 3) advance_patch();
+            if constexpr (tap == G::PT - 1) advance_patch();
           }
           if constexpr (tap == 1)
             if (after_tile) store_tile(t - 1);
-          if constexpr (RES && tap >= 2 && tap <= 5)
+          if constexpr (RES && tap >= 2 && tap < 2 + G::RT)
             if (last_chunk) res_pieces(t, tap);
         }
       }
@@ -350,6 +354,244 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (!wloader) store_tile(tp_end - 1);
+}
+
+
+// ---------------------------------------------------------------------------
+// Resident-weight halo conv (variant 25): Cin = Cout = 64 (layer1).
+//
+// All 9 taps' weights (64 x 576 bf16 = 72 KB) are DMA'd into LDS once per
+// workgroup, so a tile's 9 K-steps need no weight ring and no barrier: the
+// only synchronisation is ONE barrier per 16x16 tile, which publishes the
+// next tile's (double-buffered) input patch.  Within a tile, tap k+1's
+// fragments are read while tap k's MFMAs run (no barrier in between).  The
+// residual comes straight from global memory into registers (prefetched during
+// the tile) and the epilogue stores from registers (8 B per lane), so LDS holds
+// only weights + 2 patches (72 + 2 x 41 KB).
+//
+// The epilogue is staggered across the two waves of each SIMD (waves w, w+4):
+// waves 0-3 run theirs before the tile barrier, waves 4-7 after it, so one
+// wave's VALU epilogue overlaps its partner's MFMAs instead of idling the
+// SIMD's matrix pipe.
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
+  constexpr int NW = 8, TC = 4, TP = 2, TW = 16, TH = 16;
+  constexpr int PW = TW + 2, PR = PW * (TH + 2);  // 18 x 18 patch rows
+  constexpr int NDP = (PR + 7) / 8;               // 41 DMA pieces per patch
+  constexpr int QP = (NDP + NW - 1) / NW;         // <= 6 per wave
+  constexpr int WBYTES = 9 * 64 * 128;            // resident weights
+  constexpr int PATCH = NDP * 1024;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool early = wave < 4;  // epilogue before the tile barrier
+  const int wp = wave;          // tile rows 2wp, 2wp+1; all 64 channels
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles_x = a.W / TW, tiles_img = tiles_x * (a.H / TH);
+  const int tiles_p = a.N * tiles_img;
+  const int tp_begin = (int)((int64_t)w * tiles_p / gridDim.x), tp_end = (int)((int64_t)(w + 1) * tiles_p / gridDim.x);
+  if (tp_begin >= tp_end) return;
+
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, (int)a.wt_bytes, 0x00020000);
+  const int ps0 = (int)a.in0_pstride * 2;
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+  // ---- patch pieces of tile `pt` into buffer `pb` (piece q = wave + 8k, rows 8q..8q+7)
+  int poff[QP];
+  auto prep_patch = [&](int pt) __attribute__((always_inline)) {
+    const int b = pt / tiles_img, rem = pt - b * tiles_img;
+    const int oy0 = (rem / tiles_x) * TH, ox0 = (rem % tiles_x) * TW;
+#pragma unroll
+    for (int k = 0; k < QP; ++k) {
+      const int pr = 8 * (wave + NW * k) + (lane >> 3);
+      const int py = pr / PW, px = pr - py * PW;
+      const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+      poff[k] = (pr < PR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+                    ? ((b * a.H + iy) * a.W + ix) * ps0 + ((lane & 7) ^ (pr & 6)) * 16
+                    : 0x7FFFFFF0;
+    }
+  };
+  auto patch_piece = [&](int k, int pb) __attribute__((always_inline)) {
+    if (NDP % NW == 0 || wave + NW * k < NDP)
+      dma16_m0(r0, poff[k], lds0 + WBYTES + pb * PATCH + (wave + NW * k) * 1024);
+  };
+
+  // ---- prologue: resident weights (72 pieces, 9 per wave) + the first patch
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int q = wave + NW * i;  // tap q / 8, rows 8 (q % 8) + lane / 8
+    const int tap = q >> 3, co = 8 * (q & 7) + (lane >> 3);
+    dma16_m0(rw, co * (a.wt_ld * 2) + tap * 128 + ((lane & 7) ^ (co & 6)) * 16, lds0 + tap * 8192 + (q & 7) * 1024);
+  }
+  prep_patch(tp_begin);
+#pragma unroll
+  for (int k = 0; k < QP; ++k) patch_piece(k, 0);
+  if (tp_begin + 1 < tp_end) prep_patch(tp_begin + 1);
+
+  float bias[TC][4];
+#pragma unroll
+  for (int i = 0; i < TC; ++i) {
+    const float4 b4 = *(const float4*)(a.bias + i * 16 + (lane >> 4) * 4);
+    bias[i][0] = b4.x; bias[i][1] = b4.y; bias[i][2] = b4.z; bias[i][3] = b4.w;
+  }
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint2 resv[TC][TP];
+
+  const int fr = lane & 15, fg = lane >> 4;
+  // lane's pixel of fragment j: tile row 2wp + j, column fr; channels i*16 + fg*4 .. +3
+  auto pix_index = [&](int t, int j) __attribute__((always_inline)) {
+    const int b = t / tiles_img, rem = t - b * tiles_img;
+    const int oy = (rem / tiles_x) * TH + 2 * wp + j, ox = (rem % tiles_x) * TW + fr;
+    return (int64_t)(b * a.Ho + oy) * a.Wo + ox;
+  };
+  auto load_res = [&](int t, int j) __attribute__((always_inline)) {
+    if constexpr (RES) {
+      const u16* rp = (const u16*)a.res + pix_index(t, j) * a.res_pstride + fg * 4;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) resv[i][j] = *(const uint2*)(rp + i * 16);
+    }
+  };
+  auto epilogue = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      u16* op = (u16*)a.out + pix_index(t, j) * a.out_pstride + fg * 4;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[i][r];
+        if constexpr (RES) {
+          v[0] += __uint_as_float(resv[i][j].x << 16);
+          v[1] += __uint_as_float(resv[i][j].x & 0xFFFF0000u);
+          v[2] += __uint_as_float(resv[i][j].y << 16);
+          v[3] += __uint_as_float(resv[i][j].y & 0xFFFF0000u);
+        }
+        if constexpr (RELU)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        uint2 q;
+        q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *(uint2*)(op + i * 16) = q;
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  // fragments of tap k (both K-halves) from resident weights + patch buffer pb
+  auto read_tap = [&](uint4 (&wf)[2][TC], uint4 (&pf)[2][TP], int k, int pb) __attribute__((always_inline)) {
+    const char* wb = smem + k * 8192;
+    const char* pbuf = smem + WBYTES + pb * PATCH;
+    const int ky = k / 3, kx = k - ky * 3;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = fg + 4 * s;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const int r = i * 16 + fr;
+        wf[s][i] = *(const uint4*)(wb + r * 128 + (hswz(r, c) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int r = (2 * wp + j + ky) * PW + kx + fr;
+        pf[s][j] = *(const uint4*)(pbuf + r * 128 + (hswz(r, c) << 4));
+      }
+    }
+  };
+  auto mma_tap = [&](const uint4 (&wf)[2][TC], const uint4 (&pf)[2][TP]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) mfma_chunk<u16>(wf[s][i], pf[s][j], acc[i][j]);
+  };
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  uint4 wf[2][2][TC], pf[2][2][TP];
+  int pb = 0;
+  for (int t = tp_begin; t < tp_end; ++t) {
+    const bool has_next = t + 1 < tp_end;
+    read_tap(wf[0], pf[0], 0, pb);
+    static_for<9>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      // next tile's patch: one piece per tap over taps 0..QP-1; this tile's
+      // residual: fragment j at tap 1 + j
+      if constexpr (k < QP)
+        if (has_next) patch_piece(k, pb ^ 1);
+      if constexpr (k >= 1 && k <= TP) load_res(t, k - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (k < 8) {
+        read_tap(wf[(k + 1) & 1], pf[(k + 1) & 1], k + 1, pb);
+        mma_tap(wf[k & 1], pf[k & 1]);
+        // the next tap's 12 reads spread over this tap's 16 MFMAs
+#pragma unroll
+        for (int q = 0; q < 2 * (TC + TP); ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * TC * TP - 2 * (TC + TP), 0);
+      } else {
+        mma_tap(wf[k & 1], pf[k & 1]);
+      }
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    if (has_next) prep_patch(t + 2 < tp_end ? t + 2 : t + 1);
+    // early waves: epilogue, then wait for their DMAs/loads (the stores, youngest, may stay in flight)
+    if (early) {
+      epilogue(t);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TC * TP) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (!early) epilogue(t);
+    pb ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool RES, bool RELU>
+static int launch_halo_rw_t(const BlockConvArgs& a, hipStream_t s) {
+  constexpr int smem = 9 * 64 * 128 + 2 * 41 * 1024;
+  static_assert(smem <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)halo_rw_kernel<RES, RELU>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              smem);
+    attr = true;
+  }
+  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.in1,
+              "halo conv: 3x3, stride 1, pad 1, no GEMM shortcut");
+  SAD_REQUIRE(a.Cin == 64 && a.Cout == 64, "resident-weight halo conv (variant 25): Cin = Cout = 64");
+  SAD_REQUIRE(a.W % 16 == 0 && a.H % 16 == 0 && a.Ho == a.H && a.Wo == a.W, "image must tile exactly");
+  SAD_REQUIRE(a.wt_ld >= 9 * a.Cin && (a.wt_ld * 2) % 16 == 0, "weight row length");
+  SAD_REQUIRE(!a.res || a.res_pstride >= a.Cout, "residual pixel stride");
+  SAD_REQUIRE(a.out_pstride % 4 == 0 && (!a.res || a.res_pstride % 4 == 0), "8-B aligned pixel rows");
+  const int64_t tiles_p = (int64_t)a.N * (a.H / 16) * (a.W / 16);
+  SAD_REQUIRE(tiles_p < (1ll << 31) && (int64_t)a.N * a.H * a.W * a.in0_pstride * 2 < (1ll << 31),
+              "too large for one launch");
+  const int64_t g = std::min<int64_t>(tiles_p, 256);
+  hipLaunchKernelGGL((halo_rw_kernel<RES, RELU>), dim3((unsigned)g), dim3(512), smem, s, a);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
+}
+
+int launch_halo_rw(const BlockConvArgs& a, hipStream_t s) {
+  if (a.res) return a.relu ? launch_halo_rw_t<true, true>(a, s) : launch_halo_rw_t<true, false>(a, s);
+  return a.relu ? launch_halo_rw_t<false, true>(a, s) : launch_halo_rw_t<false, false>(a, s);
 }
 
 template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU>
@@ -390,9 +632,11 @@ static int launch_halo_g(const BlockConvArgs& a, hipStream_t s) {
 
 // Variants (channels x tile (TH x TW), waves, wave tile, LDS; one WG per CU):
 //  20: 64 x 16x16  8w  64x32  154 KB
+//  21: 64 x 16x16  4w  64x64  156 KB (one wave per SIMD: half the LDS fragment reads per MFMA)
 int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s) {
   switch (v) {
     case 20: return launch_halo_g<1, 8, 4, 2, 16>(a, s);
+    case 21: return launch_halo_g<1, 4, 4, 4, 16>(a, s);
   }
   set_error("unknown halo-conv variant");
   return SAD_ERR_ARG;

@@ -1,0 +1,95 @@
+"""GPU numerics of every block-conv tile variant (libsad block.hip / halo.hip)
+against a plain torch fp32 conv of the same bf16-rounded operands.
+
+One launch computes  act(conv3x3(x) [+ 1x1 shortcut(sc)] + bias [+ res])  -- the
+BasicBlock halves of timm resnet18 (inference_runner.py:49-51).
+The kernels accumulate in fp32 and round the output once to bf16, so the bar is
+|out - ref| <= 1 bf16 ulp of |ref| (2^-8 relative) + a 1e-2 absolute floor for
+summation-order noise near zero.  Variants of one kernel family sum K in the
+same order, so their outputs must also agree bit for bit.
+
+Shapes cover: several tiles per persistent workgroup, a ragged last pixel tile
+(M % tile != 0), images smaller than one workgroup's pixel tile, the identity
+shortcut as MFMA columns and as an epilogue residual, the strided downsample.
+"""
+import zlib
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+
+def _ref(x, w, bias, stride, sc, sc_stride, res, relu, k=3):
+    """fp32 NCHW reference of the block-conv contract on the bf16 operands."""
+    cin = x.shape[3]
+    wc = w[:, :k * k * cin].float().reshape(w.shape[0], k, k, cin).permute(0, 3, 1, 2)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), wc, stride=stride, padding=k // 2)
+    if sc is not None:
+        w1 = w[:, k * k * cin:k * k * cin + sc.shape[3]].float()
+        s = sc.float()[:, ::sc_stride, ::sc_stride, :]
+        y = y + torch.einsum('nhwc,oc->nohw', s, w1)
+    y = y + bias.view(1, -1, 1, 1)
+    if res is not None:
+        y = y + res.float().permute(0, 3, 1, 2)
+    if relu:
+        y = y.clamp_min(0)
+    return y.permute(0, 2, 3, 1)
+
+
+def _check(out, ref):
+    d = (out.float() - ref).abs()
+    bound = ref.abs() * 2.0 ** -8 + 1e-2
+    assert bool((d <= bound).all()), f'max |d| {d.max().item():.3g}, worst excess {(d - bound).max().item():.3g}'
+
+
+# name, N, H, Cin, Cout, stride, shortcut ('id' | 'ds' | 'res' | None), variants
+CASES = [
+    ('l1-res', 5, 128, 64, 64, 1, 'res', [20, 21, 25]),  # 320 tiles: 2 per workgroup on some
+    ('l1-plain', 2, 48, 64, 64, 1, None, [9, 11, 16, 20, 25]),
+    ('l2-res', 2, 32, 128, 128, 1, 'res', [20, 21]),
+    ('l2-s2', 3, 34, 64, 128, 2, None, [10, 12, 14, 15, 18, 23]),
+    ('l2-ds', 2, 16, 128, 128, 1, 'ds', [10, 12, 14, 15, 18, 23]),
+    ('l3-id', 3, 14, 256, 256, 1, 'id', [13, 17, 22, 24, 10]),
+    ('l3-s2', 2, 18, 128, 256, 2, None, [13, 17, 22, 24]),
+    ('l4-ds', 5, 6, 512, 512, 1, 'ds', [13, 17, 22, 24]),
+]
+
+
+@pytest.mark.parametrize('name,N,H,Cin,Cout,stride,sc,variants', CASES, ids=[c[0] for c in CASES])
+def test_block_conv_variants(name, N, H, Cin, Cout, stride, sc, variants):
+    from sad.engine import block_conv
+    g = torch.Generator().manual_seed(zlib.crc32(name.encode()))
+    Ho = H // stride if stride == 2 else H
+    cin0 = Cin
+    scx = res = None
+    cin1 = 0
+    if sc == 'id':
+        scx = torch.randn(N, Ho, Ho, Cout, generator=g).to(torch.bfloat16)
+        cin1 = Cout
+    elif sc == 'ds':
+        scx = torch.randn(N, 2 * Ho, 2 * Ho, Cin, generator=g).to(torch.bfloat16)
+        cin0, cin1 = Cout, Cin
+        H = Ho
+    elif sc == 'res':
+        res = torch.randn(N, Ho, Ho, Cout, generator=g).to(torch.bfloat16)
+    x = torch.randn(N, H, H, cin0, generator=g).to(torch.bfloat16)
+    K = 9 * cin0 + cin1
+    w = (torch.randn(Cout, K, generator=g) * (2.0 / K) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(Cout, generator=g) * 0.1
+    ref = _ref(x, w, bias, 1 if sc == 'ds' else stride, scx, 2 if sc == 'ds' else 1, res, True)
+    xd, wd, bd = x.to(DEV), w.to(DEV), bias.to(DEV)
+    scd = scx.to(DEV) if scx is not None else None
+    rd = res.to(DEV) if res is not None else None
+    first = None
+    for v in variants:
+        out = block_conv(xd, wd, bd, 1 if sc == 'ds' else stride, 1, sc=scd, sc_stride=2 if sc == 'ds' else 1,
+                         relu=True, variant=v, res=rd)
+        torch.cuda.synchronize()
+        _check(out.cpu(), ref)
+        if first is None:
+            first = out
+        else:
+            assert torch.equal(out, first), f'variant {v} differs bitwise from variant {variants[0]}'

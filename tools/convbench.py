@@ -88,6 +88,7 @@ def main():
 
 BLOCKS = [  # name, H(in), Cin, Cout, stride, shortcut
     ('l1.c2+id', 128, 64, 64, 1, 'id'),
+    ('l1.c1', 128, 64, 64, 1, None),
     ('l2.c1', 128, 64, 128, 2, None),
     ('l2.c2+ds', 64, 128, 128, 1, 'ds'),
     ('l2.c2+id', 64, 128, 128, 1, 'id'),
@@ -123,13 +124,13 @@ def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,)):
             stride = s if sc is None else 1
             flop = 2.0 * mb * Ho * Ho * Cout * K
             ref = None
-            bc = {9: 64, 10: 128, 11: 64, 12: 128, 13: 256, 14: 128, 15: 128, 16: 64, 17: 256, 18: 128, 20: 64}
+            bc = {9: 64, 10: 128, 11: 64, 12: 128, 13: 256, 14: 128, 15: 128, 16: 64, 17: 256, 18: 128, 20: 64, 21: 64, 22: 256, 23: 128, 24: 256, 25: 64}
             for v0 in [v + (ab << 8) for v in variants for ab in ablate]:
                 v = v0 & 255
-                if Cout % bc[v] or (v == 20 and (stride != 1 or sc == 'ds')):
+                if Cout % bc[v] or (v in (20, 21, 25) and (stride != 1 or sc == 'ds')) or (v == 25 and Cout != 64):
                     continue
                 # the halo kernel (20) takes the identity shortcut as an epilogue residual
-                kw = dict(res=scx) if v == 20 else dict(sc=scx, sc_stride=2 if sc == 'ds' else 1)
+                kw = dict(res=scx) if v in (20, 21, 25) else dict(sc=scx, sc_stride=2 if sc == 'ds' else 1)
 
                 def run(o=None):
                     return block_conv(x, w, bias, stride, 1, relu=True, variant=v0, out=o, **kw)
