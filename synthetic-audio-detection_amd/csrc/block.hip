@@ -35,8 +35,17 @@ namespace sad {
 // WC x WP waves; each wave owns (16*TC) channels x (16*TP) pixels (TC, TP 16x16
 // MFMA tiles); OCC = workgroups per CU the LDS budget admits.
 template <int WC, int WP, int TC, int TP, int S>
-constexpr int block_smem_bytes() {
+constexpr int block_ring_bytes() {
   return S * (16 * TP * WP + 16 * TC * WC) * 128;
+}
+// the tile's bias rides behind the ring when OCC workgroups still fit a CU
+template <int WC, int WP, int TC, int TP, int S, int OCC>
+constexpr bool block_lds_bias() {
+  return (block_ring_bytes<WC, WP, TC, TP, S>() + 16 * TC * WC * 4) * OCC <= 160 * 1024;
+}
+template <int WC, int WP, int TC, int TP, int S, int OCC>
+constexpr int block_smem_bytes() {
+  return block_ring_bytes<WC, WP, TC, TP, S>() + (block_lds_bias<WC, WP, TC, TP, S, OCC>() ? 16 * TC * WC * 4 : 0);
 }
 
 template <typename T, int WC, int WP, int TC, int TP, int S, int OCC>
@@ -57,15 +66,18 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   const int w = xcd_remap(blockIdx.x, gridDim.x);
   const int tc = w % n_tc;
   const int gp = gridDim.x / n_tc, wi = w / n_tc;
-  const int64_t tiles_p = (a.M + BP - 1) / BP;
-  const int64_t tp_begin = wi * tiles_p / gp, tp_end = (wi + 1) * tiles_p / gp;
+  // 32-bit tile/pixel arithmetic (the launcher checks M + BP and the step count
+  // fit): the per-tile pixel decomposition is 2 x QP 32-bit divisions
+  const int M = (int)a.M;
+  const int tiles_p = (M + BP - 1) / BP;
+  const int tp_begin = (int)((int64_t)wi * tiles_p / gp), tp_end = (int)((int64_t)(wi + 1) * tiles_p / gp);
   if (tp_begin >= tp_end) return;  // whole workgroup (uniform)
   const int c0 = tc * BC;
 
   const int nk0 = a.KH * a.KW * a.Cin * ES / 128;
   const int nk1 = a.in1 ? a.Cin1 * ES / 128 : 0;
   const int nk = nk0 + nk1;
-  const int64_t total = (tp_end - tp_begin) * nk;
+  const int total = (tp_end - tp_begin) * nk;
 
   const __amdgpu_buffer_rsrc_t r0 =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
@@ -89,21 +101,21 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
 
   // ---- issue-side state: pixel-row metadata of the tile being DMA'd
   int poff0[QP], poff1[QP], piy[QP], pix[QP];
-  int64_t itile = tp_begin;
+  int itile = tp_begin;
   // K cursor of the next DMA, kept incrementally (no scalar divisions per step):
   // step iks = (ky * KW + kx) * kpt + ci of the conv taps, then the shortcut
   int iks = 0, ici = 0, ikx = 0, iky = 0, itoff = 0;
   const int kpt = a.Cin * ES / 128;  // K-steps per tap
-  auto set_tile = [&](int64_t tp) __attribute__((always_inline)) {
+  auto set_tile = [&](int tp) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < QP; ++i) {
       const int r = 8 * (wave + NW * i) + lrow;
       const int c = (lane & 7) ^ ((r >> 1) & 7);
-      const int64_t m = tp * BP + r;
-      if (m < a.M) {
-        const int b = (int)(m / HoWo);
-        const int rem = (int)(m - (int64_t)b * HoWo);
-        const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
+      const int m = tp * BP + r;
+      if (m < M) {
+        const int b = (int)((unsigned)m / (unsigned)HoWo);
+        const int rem = m - b * HoWo;
+        const int oy = (int)((unsigned)rem / (unsigned)a.Wo), ox = rem - oy * a.Wo;
         piy[i] = oy * a.stride - a.pad;
         pix[i] = ox * a.stride - a.pad;
         poff0[i] = ((b * a.H + piy[i]) * a.W + pix[i]) * ps0 + c * 16;
@@ -117,6 +129,12 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
     }
   };
   set_tile(itile);
+  // the tile's bias, behind the ring stages (published by the first barrier);
+  // epilogues read it from LDS: a global load there would put a vmcnt wait on
+  // whatever reuses its registers in the next K-step
+  constexpr bool LDS_BIAS = block_lds_bias<WC, WP, TC, TP, S, OCC>();
+  const float* s_bias = LDS_BIAS ? (const float*)(smem + S * STAGE) : a.bias + c0;
+  if (LDS_BIAS && tid < BC / 4) *(float4*)(smem + S * STAGE + 16 * tid) = *(const float4*)(a.bias + c0 + 4 * tid);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   auto issue = [&](int st) __attribute__((always_inline)) {
     const unsigned sb = lds0 + st * STAGE;
@@ -160,9 +178,9 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   issue(0);
   if (S == 3 && total > 1) issue(1);
   int st = 0, cks = 0;
-  int64_t ctile = tp_begin;
+  int ctile = tp_begin;
   T* __restrict__ out = (T*)a.out;
-  for (int64_t g = 0; g < total; ++g) {
+  for (int g = 0; g < total; ++g) {
     // retire this wave's DMA for step g (S = 3: step g+1's stays in flight;
     // epilogue stores issued since are waited for conservatively), then the
     // barrier publishes every wave's step-g data and frees the stage the next
@@ -242,14 +260,14 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
       // ---- register epilogue: lane holds channels co..co+3 of pixel px
       cks = 0;
       // bias of this lane's channels c0 + wc*16*TC + i*16 + fg*4 + r, re-read per
-      // tile (L2-resident) rather than held in 4*TC registers through the loop
+      // tile from LDS rather than held in 4*TC registers through the loop
       float4 bias[TC];
 #pragma unroll
-      for (int i = 0; i < TC; ++i) bias[i] = *(const float4*)(a.bias + c0 + wc * 16 * TC + i * 16 + fg * 4);
+      for (int i = 0; i < TC; ++i) bias[i] = *(const float4*)(s_bias + wc * 16 * TC + i * 16 + fg * 4);
 #pragma unroll
       for (int j = 0; j < TP; ++j) {
-        const int64_t px = ctile * BP + wp * 16 * TP + j * 16 + fr;
-        if (px < a.M) {
+        const int px = ctile * BP + wp * 16 * TP + j * 16 + fr;
+        if (px < M) {
 #pragma unroll
           for (int i = 0; i < TC; ++i) {
             const int co = c0 + wc * 16 * TC + i * 16 + fg * 4;
@@ -260,7 +278,7 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
               v[r] = acc[i][j][r] + bb[r];
               if (a.relu) v[r] = fmaxf(v[r], 0.f);
             }
-            T* op = out + px * a.out_pstride + co;
+            T* op = out + (int64_t)px * a.out_pstride + co;
             if constexpr (sizeof(T) == 2) {
               uint2 q;
               q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -284,7 +302,7 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
 
 template <typename T, int WC, int WP, int TC, int TP, int S, int OCC>
 static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
-  constexpr int smem = block_smem_bytes<WC, WP, TC, TP, S>();
+  constexpr int smem = block_smem_bytes<WC, WP, TC, TP, S, OCC>();
   static_assert(smem * OCC <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
@@ -299,257 +317,14 @@ static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
   const int64_t tiles_p = (a.M + BP - 1) / BP;
   int64_t g = std::min<int64_t>(tiles_p * n_tc, (int64_t)256 * occupancy);
   g = std::max<int64_t>(n_tc, g / n_tc * n_tc);
+  const int64_t nk = (int64_t)a.KH * a.KW * a.Cin * sizeof(T) / 128 + (a.in1 ? a.Cin1 * sizeof(T) / 128 : 0);
+  SAD_REQUIRE(a.M + BP < (1ll << 31) && (tiles_p / (g / n_tc) + 1) * nk < (1ll << 31),
+              "block conv: too many pixels for one launch (lower the micro-batch)");
   hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC>), dim3((unsigned)g), dim3(64 * WC * WP), smem, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }
 
-
-// ---------------------------------------------------------------------------
-// Mid-step-barrier variant (bf16): one wave per SIMD, each wave a 16*TC x 16*TP
-// tile with BOTH K-halves' fragments double-buffered in registers.  The ring's
-// barrier sits between the two halves of step g: before it a wave has issued
-// half 0's MFMAs and read half 1's fragments (lgkmcnt(0)) and its own DMA of
-// step g+1 has landed (vmcnt); after it the wave DMAs step g+2 into the stage
-// step g used and issues half 1's MFMAs while reading half 0 of step g+1 from
-// the other stage.  So no wave ever waits on an LDS read after a barrier: the
-// MFMA stream only pauses for the barrier's skew (vs. the two-waves-per-SIMD
-// kernel above, whose waves all read their first fragments right after it).
-template <int WC, int WP, int TC, int TP>
-__global__ __launch_bounds__(64 * WC * WP, 1) void block_mid_kernel(BlockConvArgs a) {
-  using T = u16;
-  constexpr int NW = WC * WP;
-  constexpr int BC = 16 * TC * WC, BP = 16 * TP * WP;
-  constexpr int ES = 2;
-  constexpr int STAGE = (BP + BC) * 128;
-  constexpr int QP = BP / 8 / NW, QW = BC / 8 / NW;
-  constexpr int NST = TC * TP;                  // epilogue stores per lane
-  constexpr int VST = NST < 63 ? NST : 63;      // vmcnt field limit
-  static_assert(QP * 8 * NW == BP && QW * 8 * NW == BC, "tile/wave mismatch");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wc = wave / WP, wp = wave % WP;
-  const int n_tc = a.Cout / BC;
-  const int w = xcd_remap(blockIdx.x, gridDim.x);
-  const int tc = w % n_tc;
-  const int gp = gridDim.x / n_tc, wi = w / n_tc;
-  const int64_t tiles_p = (a.M + BP - 1) / BP;
-  const int64_t tp_begin = wi * tiles_p / gp, tp_end = (wi + 1) * tiles_p / gp;
-  if (tp_begin >= tp_end) return;
-  const int c0 = tc * BC;
-
-  const int nk0 = a.KH * a.KW * a.Cin * ES / 128;
-  const int nk1 = a.in1 ? a.Cin1 * ES / 128 : 0;
-  const int nk = nk0 + nk1;
-  const int64_t total = (tp_end - tp_begin) * nk;
-
-  const __amdgpu_buffer_rsrc_t r0 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t r1 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(a.in1 ? a.in1 : a.in0), (short)0, (int)a.in1_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, (int)a.wt_bytes, 0x00020000);
-  const int ps0 = (int)a.in0_pstride * ES, ps1 = (int)a.in1_pstride * ES;
-  const int HoWo = a.Ho * a.Wo;
-  const int lrow = lane >> 3;
-
-  const int ktot_b = a.wt_ld * ES;
-  int woff[QW];
-#pragma unroll
-  for (int i = 0; i < QW; ++i) {
-    const int r = 8 * (wave + NW * i) + lrow;
-    const int c = (lane & 7) ^ (((BP + r) >> 1) & 7);
-    woff[i] = (c0 + r) * ktot_b + c * 16;
-  }
-  int poff0[QP], poff1[QP], piy[QP], pix[QP];
-  int64_t itile = tp_begin;
-  int iks = 0;
-  auto set_tile = [&](int64_t tp) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < QP; ++i) {
-      const int r = 8 * (wave + NW * i) + lrow;
-      const int c = (lane & 7) ^ ((r >> 1) & 7);
-      const int64_t m = tp * BP + r;
-      if (m < a.M) {
-        const int b = (int)(m / HoWo);
-        const int rem = (int)(m - (int64_t)b * HoWo);
-        const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
-        piy[i] = oy * a.stride - a.pad;
-        pix[i] = ox * a.stride - a.pad;
-        poff0[i] = ((b * a.H + piy[i]) * a.W + pix[i]) * ps0 + c * 16;
-        poff1[i] = ((b * a.H1 + oy * a.ss1) * a.W1 + ox * a.ss1) * ps1 + c * 16;
-      } else {
-        piy[i] = -0x4000;
-        pix[i] = -0x4000;
-        poff0[i] = 0;
-        poff1[i] = 0x7FFF0000;
-      }
-    }
-  };
-  set_tile(itile);
-  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  auto issue = [&](int st) __attribute__((always_inline)) {
-    const unsigned sb = lds0 + st * STAGE;
-    if (iks < nk0) {
-      const int kpt = a.Cin * ES / 128;
-      const int tap = iks / kpt;
-      const int ci = iks - tap * kpt;
-      const int ky = tap / a.KW, kx = tap - ky * a.KW;
-      const int toff = (ky * a.W + kx) * ps0 + ci * 128;
-#pragma unroll
-      for (int i = 0; i < QP; ++i) {
-        const int iy = piy[i] + ky, ix = pix[i] + kx;
-        const bool ok = ((unsigned)iy < (unsigned)a.H) && ((unsigned)ix < (unsigned)a.W);
-        dma16_m0(r0, ok ? poff0[i] + toff : 0x7FFFFFF0, sb + (wave + NW * i) * 1024);
-      }
-    } else {
-      const int toff = (iks - nk0) * 128;
-#pragma unroll
-      for (int i = 0; i < QP; ++i) dma16_m0(r1, poff1[i] + toff, sb + (wave + NW * i) * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < QW; ++i) dma16_m0(rw, woff[i] + iks * 128, sb + BP * 128 + (wave + NW * i) * 1024);
-    if (++iks == nk) {
-      iks = 0;
-      if (++itile < tp_end) set_tile(itile);
-    }
-  };
-
-  f32x4 acc[TC][TP];
-#pragma unroll
-  for (int i = 0; i < TC; ++i)
-#pragma unroll
-    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fg = lane >> 4;
-  auto read_half = [&](uint4 (&wf)[TC], uint4 (&pf)[TP], int stg, int s) __attribute__((always_inline)) {
-    const char* base = smem + stg * STAGE;
-    const int c = fg + 4 * s;
-#pragma unroll
-    for (int i = 0; i < TC; ++i) {
-      const int r = BP + wc * 16 * TC + i * 16 + fr;
-      wf[i] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
-    }
-#pragma unroll
-    for (int j = 0; j < TP; ++j) {
-      const int r = wp * 16 * TP + j * 16 + fr;
-      pf[j] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
-    }
-  };
-  auto mma_half = [&](const uint4 (&wf)[TC], const uint4 (&pf)[TP]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < TC; ++i)
-#pragma unroll
-      for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pf[j], acc[i][j]);
-  };
-  // the other half's TC+TP fragment reads spread over the first 2(TC+TP) MFMAs
-  auto interleave = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < TC + TP; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, TC * TP - 2 * (TC + TP), 0);
-  };
-  static_assert(TC * TP >= 2 * (TC + TP), "interleave pattern");
-
-  issue(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (total > 1) issue(1);
-  uint4 w0[TC], p0[TP], w1[TC], p1[TP];
-  read_half(w0, p0, 0, 0);
-  int st = 0, cks = 0;
-  bool stored = false;
-  int64_t ctile = tp_begin;
-  T* __restrict__ out = (T*)a.out;
-  for (int64_t g = 0; g < total; ++g) {
-    __builtin_amdgcn_sched_barrier(0);
-    read_half(w1, p1, st, 1);
-    mma_half(w0, p0);
-    interleave();
-    __builtin_amdgcn_sched_barrier(0);
-    // this wave's DMA of step g+1 (older than any epilogue stores) has landed;
-    // its half-1 reads of stage st are done -> the barrier publishes step g+1
-    // and frees stage st
-    if (!(a.ablate & 2)) {
-      if (stored)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VST) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!(a.ablate & 4)) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    stored = false;
-    if (g + 2 < total && !(a.ablate & 1)) issue(st);
-    __builtin_amdgcn_sched_barrier(0);
-    read_half(w0, p0, st ^ 1, 0);  // step g+1 (stale, unused, past the last step)
-    mma_half(w1, p1);
-    interleave();
-    __builtin_amdgcn_sched_barrier(0);
-    st ^= 1;
-    if (++cks == nk) {
-      cks = 0;
-      // bias re-read per tile (L2-resident) instead of held in 4*TC registers
-      float4 bias[TC];
-#pragma unroll
-      for (int i = 0; i < TC; ++i) bias[i] = *(const float4*)(a.bias + c0 + wc * 16 * TC + i * 16 + fg * 4);
-#pragma unroll
-      for (int j = 0; j < TP; ++j) {
-        const int64_t px = ctile * BP + wp * 16 * TP + j * 16 + fr;
-        if (px < a.M) {
-#pragma unroll
-          for (int i = 0; i < TC; ++i) {
-            const int co = c0 + wc * 16 * TC + i * 16 + fg * 4;
-            float v[4];
-            const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              v[r] = acc[i][j][r] + bb[r];
-              if (a.relu) v[r] = fmaxf(v[r], 0.f);
-            }
-            uint2 q;
-            q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-            q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-            __builtin_nontemporal_store(q.x, (uint32_t*)(out + px * a.out_pstride + co));
-            __builtin_nontemporal_store(q.y, (uint32_t*)(out + px * a.out_pstride + co) + 1);
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < TC; ++i)
-#pragma unroll
-        for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      ++ctile;
-      stored = true;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <int WC, int WP, int TC, int TP>
-static int launch_mid_t(const BlockConvArgs& a, hipStream_t s) {
-  constexpr int smem = block_smem_bytes<WC, WP, TC, TP, 2>();
-  static_assert(smem <= 160 * 1024, "LDS budget");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)block_mid_kernel<WC, WP, TC, TP>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
-  constexpr int BC = 16 * TC * WC, BP = 16 * TP * WP;
-  SAD_REQUIRE(a.Cout % BC == 0, "Cout must be a multiple of the channel tile");
-  const int n_tc = a.Cout / BC;
-  const int64_t tiles_p = (a.M + BP - 1) / BP;
-  int64_t g = std::min<int64_t>(tiles_p * n_tc, 256);
-  g = std::max<int64_t>(n_tc, g / n_tc * n_tc);
-  hipLaunchKernelGGL((block_mid_kernel<WC, WP, TC, TP>), dim3((unsigned)g), dim3(64 * WC * WP), smem, s, a);
-  SAD_CHECK_HIP(hipGetLastError());
-  return SAD_OK;
-}
 
 // Variants (channels x pixels tile, waves, wave tile, ring stages, LDS, workgroups/CU):
 //  9: 64x256  4w 64x64  S2  80 KB 2     10: 128x128 4w 64x64  S2  64 KB 2
@@ -557,9 +332,6 @@ static int launch_mid_t(const BlockConvArgs& a, hipStream_t s) {
 // 13: 256x256 8w 128x64 S2 128 KB 1     14: 128x256 8w 64x64  S2  96 KB 1
 // 15: 128x256 8w 64x64  S3 144 KB 1     16: 64x512  8w 64x64  S2 144 KB 1
 // 17: 256x128 4w 128x64 S2  96 KB 1     18: 128x256 4w 64x128 S2  96 KB 1
-// mid-step barrier (block_mid_kernel, bf16 only), one wave per SIMD:
-// 22: 256x256 4w 128x128 S2 128 KB      23: 128x256 4w 64x128 S2 96 KB
-// 24: 256x128 4w 128x64  S2  96 KB
 template <typename T>
 static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
   switch (v) {
@@ -598,9 +370,7 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
 static bool variant_fits(int v, int cout) {
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128};
   if (v == 20 || v == 21) return cout % 64 == 0;
-  if (v == 22 || v == 24) return cout % 256 == 0;
   if (v == 25) return cout == 64;
-  if (v == 23) return cout % 128 == 0;
   return v >= 9 && v <= 18 && cout % bc[v] == 0;
 }
 
@@ -632,12 +402,6 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
     return launch_halo_v(a, v, s);
   }
   SAD_REQUIRE(!a.res, "an epilogue residual needs the halo kernel (variant 20)");
-  if (v >= 22 && v <= 24) {
-    SAD_REQUIRE(dtype == SAD_BF16, "mid-barrier block conv (variants 22-24): bf16 only");
-    if (v == 22) return launch_mid_t<2, 2, 8, 8>(a, s);
-    if (v == 23) return launch_mid_t<2, 2, 4, 8>(a, s);
-    return launch_mid_t<2, 2, 8, 4>(a, s);
-  }
   return dtype == SAD_BF16 ? launch_block_v<u16>(a, v, s) : launch_block_v<float>(a, v, s);
 }
 

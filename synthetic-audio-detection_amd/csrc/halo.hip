@@ -200,6 +200,19 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
   // activation, bf16 -> the tile's LDS staging rows (in place over the
   // residual rows: each lane writes exactly the bytes it read)
   auto epilogue = [&]() __attribute__((always_inline)) {
+    // every residual read issued before the first in-place write (the compiler
+    // cannot prove the lanes' read and write addresses disjoint across (i, j))
+    uint2 rvs[TP][TC];
+    if constexpr (RES) {
+#pragma unroll
+      for (int j = 0; j < TP; ++j)
+#pragma unroll
+        for (int i = 0; i < TC; ++i) {
+          const int p = (wp * TP + j) * TW + fr;
+          const int cl = wc * 16 * TC + i * 16 + fg * 4;
+          rvs[j][i] = *(const uint2*)(smem + G::OFF_RES + p * 128 + (hswz(p, cl >> 3) << 4) + (cl & 7) * 2);
+        }
+    }
 #pragma unroll
     for (int j = 0; j < TP; ++j) {
       const int p = (wp * TP + j) * TW + fr;
@@ -211,7 +224,7 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[i][r];
         if constexpr (RES) {
-          const uint2 rv = *sp;
+          const uint2 rv = rvs[j][i];
           v[0] += __uint_as_float(rv.x << 16);
           v[1] += __uint_as_float(rv.x & 0xFFFF0000u);
           v[2] += __uint_as_float(rv.y << 16);

@@ -50,11 +50,11 @@ CASES = [
     ('l1-res', 5, 128, 64, 64, 1, 'res', [20, 21, 25]),  # 320 tiles: 2 per workgroup on some
     ('l1-plain', 2, 48, 64, 64, 1, None, [9, 11, 16, 20, 25]),
     ('l2-res', 2, 32, 128, 128, 1, 'res', [20, 21]),
-    ('l2-s2', 3, 34, 64, 128, 2, None, [10, 12, 14, 15, 18, 23]),
-    ('l2-ds', 2, 16, 128, 128, 1, 'ds', [10, 12, 14, 15, 18, 23]),
-    ('l3-id', 3, 14, 256, 256, 1, 'id', [13, 17, 22, 24, 10]),
-    ('l3-s2', 2, 18, 128, 256, 2, None, [13, 17, 22, 24]),
-    ('l4-ds', 5, 6, 512, 512, 1, 'ds', [13, 17, 22, 24]),
+    ('l2-s2', 3, 34, 64, 128, 2, None, [10, 12, 14, 15, 18]),
+    ('l2-ds', 2, 16, 128, 128, 1, 'ds', [10, 12, 14, 15, 18]),
+    ('l3-id', 3, 14, 256, 256, 1, 'id', [13, 17, 10]),
+    ('l3-s2', 2, 18, 128, 256, 2, None, [13, 17]),
+    ('l4-ds', 5, 6, 512, 512, 1, 'ds', [13, 17]),
 ]
 
 
