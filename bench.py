@@ -39,6 +39,8 @@ BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 DOMINANT_VARIANT = 13
 DOMINANT_KERNEL = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1>|131072'
 F32_PEAK_TFLOPS = 157.3
+FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats
+FE_BYTES = 256000 + 128512     # int16 PCM read + fp32 [128, 251] map written
 
 
 def cpu_baseline(seconds: float = 15.0):
@@ -100,11 +102,16 @@ def main():
     logits = torch.empty(B, args.heads, 2, device=dev)
     merged = torch.empty(B, args.heads + 1, device=dev)
     gathered = torch.empty(world * B, args.heads + 1, device=dev) if world > 1 else None
-    ev = []
+    ev, fev = [], []
 
     def step(timed):
+        if timed:
+            f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            f0.record()
         m = eng.frontend(pcm)
         if timed:
+            f1.record()
+            fev.append((f0, f1))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         eng.backbones[0](m, out=feats)
@@ -137,6 +144,7 @@ def main():
     _lib.call('sad_profile_end', DOMINANT_VARIANT, _lib.ctypes.byref(k_ms), _lib.ctypes.byref(k_n),
               _lib.ctypes.byref(k_fl))
     bb_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    fe_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev)
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -178,7 +186,15 @@ def main():
                                       'ms_per_step': round(bb_ms, 3), 'flop_per_segment': BACKBONE_FLOP,
                                       'what': 'fused resize+stem + 16 block-conv GEMMs + avgpool, HIP events '
                                               'around the backbone call'},
-                         'measured_gemm_ceiling_tflops': 1344.0},
+                         'measured_gemm_ceiling_tflops': 1344.0,
+                         # front end (configs[1]): fused STFT/mel/dB + standardise, fp32 VALU-bound
+                         # (16.4 MFLOP and 384,512 B per segment)
+                         'frontend': {'ms_per_step': round(fe_ms, 3),
+                                      'achieved_tflops': round(FE_FLOP * B / (fe_ms * 1e-3) / 1e12, 2),
+                                      'peak_tflops': F32_PEAK_TFLOPS,
+                                      'frac': round(FE_FLOP * B / (fe_ms * 1e-3) / 1e12 / F32_PEAK_TFLOPS, 4),
+                                      'achieved_gbps': round(FE_BYTES * B / (fe_ms * 1e-3) / 1e9, 1),
+                                      'segments_per_s': round(B / (fe_ms * 1e-3), 1)}},
         }
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline()

@@ -386,11 +386,12 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
 }
 
 // Segments per sub-chunk for the stem, layer1 and layer2 on the block path
-// (SAD_FRONT_MB; 0 = the whole micro-batch, the default: measured 42.6k seg/s at
-// 0 vs 41.4k at 32 and 38.0k at 16 -- the convs are not HBM-bound).  At
-// 32 segments a layer1 activation is 64 MiB (bf16), so a conv's input, output
-// and residual stay in the 256 MiB Infinity Cache instead of round-tripping
-// HBM; layer3/4 run on the whole micro-batch (their grids need the pixels).
+// (SAD_FRONT_MB; 0 = the whole micro-batch, the default).  At 32 segments a
+// layer1 activation is 64 MiB (bf16), so a conv's input, output and residual
+// can stay in the 256 MiB Infinity Cache; layer3/4 run on the whole micro-batch
+// (their grids need the pixels).  Measured box-dependent (tools/ab_env.sh,
+// resident-weight layer1 kernel): +1.7% on one box (46.1k vs 45.3k seg/s),
+// -1.1% on another (43.2k vs 43.6k); 16 is 7% slower (layer2 underfills).
 static int front_sub_batch() {
   static int v = [] {
     const char* e = getenv("SAD_FRONT_MB");
