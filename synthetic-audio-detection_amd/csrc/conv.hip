@@ -450,6 +450,9 @@ constexpr int STEM_P = 4;
 constexpr int STEM_BAND_ROWS = 4 * STEM_P + 8;  // 4P+7 with non-zero weights
 constexpr int STEM_BPITCH = 544;                 // bf16 elements per band row (>= 518)
 constexpr int STEM_HROWS = 10;                   // x-interpolated map rows kept in LDS
+constexpr int STEM_OPITCH = 160;                 // staging bytes per pooled pixel (64 ch bf16 + pad):
+                                                 // 40 dwords -> the 4 rows a 32-lane group writes
+                                                 // land on disjoint 8-bank sets
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
@@ -462,9 +465,9 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
   __shared__ __attribute__((aligned(16))) float s_bias[64];
   // x-interpolated map rows while the band is built; afterwards the pooled-row
   // staging [128 q][64 ch] bf16 and the wave-edge exchange [4][64] fp32
-  __shared__ __attribute__((aligned(16))) float s_u[STEM_HROWS * 512];
-  u16* s_out = (u16*)s_u;
-  float* s_edge = s_u + 128 * 64 / 2;
+  __shared__ __attribute__((aligned(16))) float s_u[STEM_HROWS * 512 + 256];
+  char* s_out = (char*)s_u;                  // pooled row staging, [128 q][STEM_OPITCH B]
+  float* s_edge = s_u + 128 * STEM_OPITCH / 4;  // [4 waves][64 ch]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int py0 = blockIdx.x * STEM_P;
@@ -571,7 +574,7 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
         av.z = *(const uint32_t*)(p + 4);
         av.w = *(const uint32_t*)(p + 6);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mfma_chunk<u16>(bw[j][s], av, r[i][j]);
+        for (int j = 0; j < 4; ++j) mfma_chunk<u16>(av, bw[j][s], r[i][j]);  // C[px][ch]
       }
     }
   };
@@ -595,42 +598,39 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) cur[i][j][e] = fmaxf(cur[i][j][e], carry[i][j][e]);
-    // wave edge: conv column 64w-1 comes from wave w-1 (its block 3, lane fr = 15)
-    if (fr == 15) {
+    // wave edge: conv column 64w-1 comes from wave w-1 (tile 3, lanes fg = 3, element 3)
+    if (fg == 3) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        *(float4*)(s_edge + wave * 64 + j * 16 + fg * 4) = make_float4(cur[3][j][0], cur[3][j][1], cur[3][j][2], cur[3][j][3]);
+      for (int j = 0; j < 4; ++j) s_edge[wave * 64 + j * 16 + fr] = cur[3][j][3];
     }
     __syncthreads();
-    // horizontal max (pooled q = 32w + 8i + fr/2 from even lanes: cols 2q-1, 2q, 2q+1),
-    // then bias, ReLU, bf16 -> staging
+    // horizontal max, window 3 stride 2.  Lane (fr, fg) of tile i holds conv
+    // columns 64w+16i+4fg+e of channel 16j+fr (C[px][ch] layout), so its pooled
+    // outputs q = 32w+8i+2fg (columns 4fg-1..4fg+1) and q+1 (4fg+1..4fg+3) are
+    // in-lane except column 4fg-1: element 3 of lane (fr, fg-1), or of tile
+    // i-1's lane (fr, 3), or of wave w-1 -- one bpermute rotating the wave by
+    // 16 lanes.  Then bias, ReLU, and channel pairs (fr, fr+1) packed by a DPP
+    // row shift: even lanes write pooled q, odd lanes q+1, as b32.
+    float bias[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bias[j] = s_bias[j * 16 + fr];
+    const bool even = (fr & 1) == 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float4 bj = *(const float4*)(s_bias + j * 16 + fg * 4);
-        const float bias[4] = {bj.x, bj.y, bj.z, bj.w};
-        float o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x = cur[i][j][e];
-          const float right = dppf<0x101>(x);  // row_shl:1  (fr + 1)
-          const float left_in = dppf<0x111>(x);  // row_shr:1  (fr - 1)
-          float left_blk;
-          if (i > 0)
-            left_blk = dppf<0x10F>(cur[i - 1][j][e]);  // row_shl:15 (lane 0 <- 15 of block i-1)
-          else
-            left_blk = wave > 0 ? s_edge[(wave - 1) * 64 + j * 16 + fg * 4 + e] : -INFINITY;
-          const float left = fr == 0 ? left_blk : left_in;
-          o[e] = fmaxf(fmaxf(fmaxf(x, right), left) + bias[e], 0.f);
-        }
-        if ((fr & 1) == 0) {
-          const int q = wave * 32 + i * 8 + (fr >> 1);
-          uint2 qv;
-          qv.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-          qv.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-          *(uint2*)(s_out + q * 64 + j * 16 + fg * 4) = qv;
-        }
+        const f32x4 x = cur[i][j];
+        const float send = fg == 3 ? (i > 0 ? cur[i - 1][j][3] : 0.f) : x[3];
+        float left = __int_as_float(__builtin_amdgcn_ds_bpermute(((lane + 48) & 63) << 2, __float_as_int(send)));
+        if (i == 0 && fg == 0) left = wave > 0 ? s_edge[(wave - 1) * 64 + j * 16 + fr] : -INFINITY;
+        const float oa = fmaxf(fmaxf(fmaxf(left, x[0]), x[1]) + bias[j], 0.f);
+        const float ob = fmaxf(fmaxf(fmaxf(x[1], x[2]), x[3]) + bias[j], 0.f);
+        const float oa_next = dppf<0x101>(oa);  // row_shl:1 (fr + 1)
+        const float ob_prev = dppf<0x111>(ob);  // row_shr:1 (fr - 1)
+        const float lo = even ? oa : ob_prev, hi = even ? oa_next : ob;
+        const int q = wave * 32 + i * 8 + 2 * fg + (even ? 0 : 1);
+        *(uint32_t*)(s_out + q * STEM_OPITCH + (j * 16 + (fr & ~1)) * 2) =
+            (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
       }
     }
     __syncthreads();
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int idx = (k * 256 + tid) * 8;  // 16 KB row, 16 B per thread per k
-      *(uint4*)(out + idx) = *(const uint4*)(s_out + idx);
+      *(uint4*)(out + idx) = *(const uint4*)(s_out + (idx >> 6) * STEM_OPITCH + (idx & 63) * 2);
     }
     __syncthreads();
   }
