@@ -385,17 +385,18 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
   return SAD_OK;
 }
 
-// Segments per sub-chunk for the stem, layer1 and layer2 on the block path
-// (SAD_FRONT_MB; 0 = the whole micro-batch, the default).  At 32 segments a
-// layer1 activation is 64 MiB (bf16), so a conv's input, output and residual
-// can stay in the 256 MiB Infinity Cache; layer3/4 run on the whole micro-batch
-// (their grids need the pixels).  Measured box-dependent (tools/ab_env.sh,
-// resident-weight layer1 kernel): +1.7% on one box (46.1k vs 45.3k seg/s),
-// -1.1% on another (43.2k vs 43.6k); 16 is 7% slower (layer2 underfills).
+// Segments per sub-chunk for the stem and layer1 on the block path
+// (SAD_FRONT_MB; 0 = the whole micro-batch).  At 32 segments a layer1
+// activation is 64 MiB (bf16), so a conv's input, output and residual can stay
+// in the 256 MiB Infinity Cache; layers 2-4 run on the whole micro-batch (their
+// grids need the pixels, and bigger launches amortise the persistent kernels'
+// ramp and tail).  Same-box sweeps (tools/frontmb_ab.sh, "front:micro-batch"):
+// 32:512 46.9k seg/s vs 0:128 45.9k, 0:512 44.4-46.4k, 64:512 45.4k; 16 is 7%
+// slower (layer2's grids underfill).  At 32:128 one box measured -1.1%.
 static int front_sub_batch() {
   static int v = [] {
     const char* e = getenv("SAD_FRONT_MB");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 32;
   }();
   return v;
 }
@@ -412,9 +413,11 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
   if (p->block_path) {
     const size_t es = p->dtype == SAD_BF16 ? 2 : 4;
     const int64_t f = front_sub_batch() > 0 ? std::min<int64_t>(front_sub_batch(), mb) : mb;
-    // stem + layer1 + layer2 per sub-chunk of f segments; layer2's output
-    // ([f, 64, 64, 128] per sub-chunk) is gathered in bufD for layers 3-4.
-    const size_t l2_elems = 64 * 64 * 128;
+    // stem + layer1 per sub-chunk of f segments (Infinity-Cache-sized); layer1's
+    // output ([f, 128, 128, 64] per sub-chunk) is gathered in bufD, then layers
+    // 2-4 run on the whole micro-batch (layer2's halo grids underfill at f = 32:
+    // its two convs took 218 + 201 vs 197 + 185 us per 128 segments).
+    const size_t l1_elems = 128 * 128 * 64;
     for (int64_t i = 0; i < mb; i += f) {
       const int64_t n = std::min(f, mb - i);
       void* a0 = bufA;
@@ -424,19 +427,20 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
       if ((rc = launch_stem(st, p->dtype, s))) return rc;
       H = 128;
       C = 64;
-      if ((rc = run_blocks(p, 0, 3, n, &a0, &a1, bufT, H, C, s))) return rc;
-      // layer2's second block writes straight into its slot of bufD
-      void* dst = (char*)bufD + (size_t)i * l2_elems * es;
+      if ((rc = run_blocks(p, 0, 1, n, &a0, &a1, bufT, H, C, s))) return rc;
+      // layer1's second block writes straight into its slot of bufD
+      void* slot = (char*)bufD + (size_t)i * l1_elems * es;
+      void* dst = slot;
       void* src = a0;
-      if ((rc = run_blocks(p, 3, 4, n, &src, &dst, bufT, H, C, s))) return rc;
-      if (src != (char*)bufD + (size_t)i * l2_elems * es) {
-        set_error("internal: layer2 output not in its bufD slot");
+      if ((rc = run_blocks(p, 1, 2, n, &src, &dst, bufT, H, C, s))) return rc;
+      if (src != slot) {
+        set_error("internal: layer1 output not in its bufD slot");
         return SAD_ERR_STATE;
       }
     }
     void* a0 = bufD;
     void* a1 = bufA;
-    if ((rc = run_blocks(p, 4, p->blocks.size(), mb, &a0, &a1, bufB, H, C, s))) return rc;
+    if ((rc = run_blocks(p, 2, p->blocks.size(), mb, &a0, &a1, bufB, H, C, s))) return rc;
     bufA = a0;
   } else {
     StemArgs st{map, img, p->mh, p->mw, p->stem_w, p->stem_b, bufA, mb};
