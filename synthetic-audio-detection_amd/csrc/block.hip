@@ -198,29 +198,49 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
     const char* base = smem + st * STAGE;
     if constexpr (TC * TP > 16) {
       // 128x64 wave tiles: 128 accumulator VGPRs leave room for one K-half's
-      // fragments only (two waves per SIMD).  The ring's DMA issue goes after
-      // half 0's fragment reads, so its SALU/VMEM issue overlaps their latency
-      // instead of delaying both waves' first MFMAs after the barrier.
+      // fragments plus half 1's pixel fragments (two waves per SIMD).  Half 1's
+      // weight fragment i is read into the registers weight fragment i of half 0
+      // frees after its TP MFMAs (rolling prefetch), so only half 0's reads,
+      // right after the barrier, expose LDS latency.  The ring's DMA issue goes
+      // after those reads and overlaps their latency.
+      uint4 wf[TC], pf[TP], pg[TP];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        uint4 wf[TC], pf[TP];
-        const int c = fg + 4 * s;
-#pragma unroll
-        for (int i = 0; i < TC; ++i) {
-          const int r = BP + wc * 16 * TC + i * 16 + fr;
-          wf[i] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
-        }
-#pragma unroll
-        for (int j = 0; j < TP; ++j) {
-          const int r = wp * 16 * TP + j * 16 + fr;
-          pf[j] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
-        }
-        if (s == 0 && do_issue) issue(ist);
-#pragma unroll
-        for (int i = 0; i < TC; ++i)
-#pragma unroll
-          for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pf[j], acc[i][j]);
+      for (int i = 0; i < TC; ++i) {
+        const int r = BP + wc * 16 * TC + i * 16 + fr;
+        wf[i] = *(const uint4*)(base + r * 128 + (swz(r, fg) << 4));
       }
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int r = wp * 16 * TP + j * 16 + fr;
+        pf[j] = *(const uint4*)(base + r * 128 + (swz(r, fg) << 4));
+      }
+      if (do_issue) issue(ist);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int r = wp * 16 * TP + j * 16 + fr;
+        pg[j] = *(const uint4*)(base + r * 128 + (swz(r, fg + 4) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+#pragma unroll
+        for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pf[j], acc[i][j]);
+        const int r = BP + wc * 16 * TC + i * 16 + fr;
+        wf[i] = *(const uint4*)(base + r * 128 + (swz(r, fg + 4) << 4));
+      }
+      // order: half 1's pixel reads, then per weight row i its TP MFMAs followed
+      // by the read of its half-1 fragment
+      __builtin_amdgcn_sched_group_barrier(0x100, TP, 0);
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pg[j], acc[i][j]);
     } else {
     if (do_issue) issue(ist);
     // both K-halves' fragments in registers; half 1's reads are issued between
