@@ -382,9 +382,18 @@ static bool halo_ok(const BlockConvArgs& a, int dtype) {
   return dtype == SAD_BF16 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.in1 && a.Cin % 64 == 0 &&
          a.Cout % 64 == 0 && a.W % 16 == 0 && a.H % 16 == 0;
 }
+// SAD_L2_HALO=0 runs layer2's second block on the implicit-GEMM kernel (identity
+// shortcut as MFMA columns) instead of the halo kernel (A/B switch)
+bool layer2_halo() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_L2_HALO");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
 int default_block_variant(const BlockConvArgs& a, int dtype) {
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
-  if (halo_ok(a, dtype) && (a.Cout <= 128 || a.res)) return 20;
+  if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo()))) return 20;
   return a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? 10 : 9);
 }
 static bool variant_fits(int v, int cout) {

@@ -62,6 +62,7 @@ int default_conv_variant(const ConvArgs& a);
 int launch_stem(const StemArgs& a, int dtype, hipStream_t s);
 int launch_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, int variant = 0);
 int default_block_variant(const BlockConvArgs& a, int dtype);
+bool layer2_halo();  // SAD_L2_HALO (default 1): layer2's identity blocks on the halo kernel
 int launch_avgpool(const void* in, int64_t B, int hw, int c, float* out, int dtype, hipStream_t s);
 int launch_heads_final(const float* y2, int64_t B, int n_heads, const float* w3, const float* b3,
                        float* logits, float* merged, hipStream_t s);
