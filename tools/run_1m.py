@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""BASELINE.json configs[3]: batched inference over a shard of 1,000,000
+synthetic 4 s segments, one process per GPU, ONE RCCL all-gather of the merged
+logits at the end.
+
+Each rank takes the contiguous range shard_range(n, rank, world) of the global
+segment ids; segments are generated on the device in chunks by the counter-hash
+PRNG (sad_synth_pcm, keyed by the GLOBAL segment id, so the result does not
+depend on the world size) -- generation is timed separately and excluded from
+the inference rate, as SURVEY 8(d) prescribes.  Prints one JSON line on rank 0.
+
+    python tools/run_1m.py [--total 1000000] [--chunk 4096]
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/run_1m.py
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'synthetic-audio-detection_amd')]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+SEG = 128000
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--total', type=int, default=1_000_000)
+    ap.add_argument('--chunk', type=int, default=4096, help='segments per device batch')
+    ap.add_argument('--heads', type=int, default=6)
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--micro-batch', type=int, default=512)
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+
+    from sad import _lib
+    from sad import weights as sw
+    from sad.distributed import gather_rows, shard_range
+    from sad.engine import Engine
+    stats = sw.load_bn_stats(os.path.join(ROOT, 'tests', 'golden', 'bn_stats_n6.npz'))
+    eng = Engine(sw.merged_state_dict(0, args.heads, False, bn_stats=stats), dev, dtype=args.dtype,
+                 micro_batch=args.micro_batch)
+    s, e = shard_range(args.total, rank, world)
+    pcm = torch.empty(args.chunk, SEG, dtype=torch.int16, device=dev)
+    local_out = torch.empty(e - s, args.heads + 1, device=dev)
+    stream = _lib.stream_handle(dev)
+
+    # warm-up (plans, workspaces) on the first chunk, untimed
+    _lib.call('sad_synth_pcm', 0, s, min(args.chunk, e - s), SEG, _lib.ptr(pcm), stream)
+    eng.forward_pcm(pcm[:min(args.chunk, e - s)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+
+    gen_s = inf_s = 0.0
+    g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    i0, i1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    for c in range(s, e, args.chunk):
+        n = min(args.chunk, e - c)
+        g0.record()
+        _lib.call('sad_synth_pcm', 0, c, n, SEG, _lib.ptr(pcm), stream)
+        g1.record()
+        i0.record()
+        _, merged = eng.forward_pcm(pcm[:n])
+        local_out[c - s:c - s + n] = merged
+        i1.record()
+        torch.cuda.synchronize()
+        gen_s += g0.elapsed_time(g1) / 1e3
+        inf_s += i0.elapsed_time(i1) / 1e3
+    t_loop = time.perf_counter() - t0
+    a0 = time.perf_counter()
+    allz = gather_rows(local_out, args.total) if world > 1 else local_out
+    torch.cuda.synchronize()
+    t_gather = time.perf_counter() - a0
+    if world > 1:
+        t = torch.tensor([inf_s, t_loop, t_gather], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        inf_s, t_loop, t_gather = t.tolist()
+    if rank == 0:
+        finite = bool(torch.isfinite(allz).all().item())
+        print(json.dumps({
+            'metric': '4s@32kHz segments/sec end-to-end (mel+ResNet+ensemble), 1M-segment shard (configs[3])',
+            'value': round(args.total / (inf_s + t_gather), 1), 'unit': 'segments/s', 'n_gpus': world,
+            'total_segments': args.total, 'chunk': args.chunk, 'dtype': args.dtype,
+            'inference_s_max_rank': round(inf_s, 3), 'allgather_s': round(t_gather, 4),
+            'synthesis_s_rank0_excluded': round(gen_s, 3), 'wall_loop_s_max_rank': round(t_loop, 3),
+            'gathered_rows': int(allz.shape[0]), 'all_finite': finite,
+            'logits_checksum': round(float(allz.double().sum().item()), 3)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()
