@@ -446,10 +446,10 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
 // row_shl:15, wave edges through LDS).  The resize is separable: map rows are
 // x-interpolated once per workgroup into LDS, then each band pixel is one
 // y-lerp (same arithmetic as bilinear512).
-constexpr int STEM_P = 4;
+constexpr int STEM_P = 8;
 constexpr int STEM_BAND_ROWS = 4 * STEM_P + 8;  // 4P+7 with non-zero weights
 constexpr int STEM_BPITCH = 544;                 // bf16 elements per band row (>= 518)
-constexpr int STEM_HROWS = 10;                   // x-interpolated map rows kept in LDS
+constexpr int STEM_HROWS = 12;                   // x-interpolated map rows kept in LDS (>= 4P+8 image rows at 128/512)
 constexpr int STEM_OPITCH = 160;                 // staging bytes per pooled pixel (64 ch bf16 + pad):
                                                  // 40 dwords -> the 4 rows a 32-lane group writes
                                                  // land on disjoint 8-bank sets
