@@ -322,8 +322,10 @@ extern "C" int sad_profile_end(int32_t variant, double* total_ms, int64_t* launc
 
 // Blocks [b0, b1) of the block path on n segments: *in (NHWC, H x H x C) ->
 // *in (the last output; the buffers *in, *alt, tmp rotate).
+// pool_out (optional): fuse the global average pool into the last block's conv2
+// when its kernel can (*pooled says whether it did; its NHWC output is not written)
 static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t n, void** in, void** alt, void* tmp,
-                      int& H, int& C, hipStream_t s) {
+                      int& H, int& C, hipStream_t s, float* pool_out = nullptr, bool* pooled = nullptr) {
   int rc;
   void* bufA = *in;
   void* bufB = *alt;
@@ -373,6 +375,11 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
       b2.bias = blk.b2;
       b2.out = bufB;
       // algorithmic work: conv2, plus the 1x1 downsample when there is one (not the identity)
+      if (pool_out && bi + 1 == b1 && block_conv_can_pool(b2, p->dtype)) {
+        b2.pool_out = pool_out;
+        b2.out = nullptr;
+        *pooled = true;
+      }
       const double fl2 = 2.0 * b2.M * b2.Cout * (9.0 * blk.cout + (blk.stride != 1 ? (double)C : 0.0));
       if ((rc = timed_block_conv(b2, p->dtype, s, fl2))) return rc;
       std::swap(bufA, bufB);
@@ -410,6 +417,7 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
   void* bufD = ws + 3 * ab;
   int rc;
   int H = 128, C = 64;
+  bool pooled = false;  // the last conv wrote the pooled features itself
   if (p->block_path) {
     const size_t es = p->dtype == SAD_BF16 ? 2 : 4;
     const int64_t f = front_sub_batch() > 0 ? std::min<int64_t>(front_sub_batch(), mb) : mb;
@@ -440,7 +448,9 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
     }
     void* a0 = bufD;
     void* a1 = bufA;
-    if ((rc = run_blocks(p, 2, p->blocks.size(), mb, &a0, &a1, bufB, H, C, s))) return rc;
+    if ((rc = run_blocks(p, 2, p->blocks.size(), mb, &a0, &a1, bufB, H, C, s, layer4_out ? nullptr : feats,
+                         &pooled)))
+      return rc;
     bufA = a0;
   } else {
     StemArgs st{map, img, p->mh, p->mw, p->stem_w, p->stem_b, bufA, mb};
@@ -518,6 +528,7 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
     const size_t es = p->dtype == SAD_BF16 ? 2 : 4;
     SAD_CHECK_HIP(hipMemcpyAsync(layer4_out, bufA, (size_t)mb * H * H * C * es, hipMemcpyDeviceToDevice, s));
   }
+  if (pooled) return SAD_OK;
   return launch_avgpool(bufA, mb, H * H, C, feats, p->dtype, s);
 }
 

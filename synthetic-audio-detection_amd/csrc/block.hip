@@ -43,9 +43,17 @@ template <int WC, int WP, int TC, int TP, int S, int OCC>
 constexpr bool block_lds_bias() {
   return (block_ring_bytes<WC, WP, TC, TP, S>() + 16 * TC * WC * 4) * OCC <= 160 * 1024;
 }
+// the fused average pool needs a [WP][BC] fp32 partial-sum area behind the bias
+// (one-workgroup-per-CU 8-wave variants)
+template <int WC, int WP, int TC, int TP, int S, int OCC>
+constexpr bool block_can_pool() {
+  return block_lds_bias<WC, WP, TC, TP, S, OCC>() && WC * WP == 8 &&
+         (block_ring_bytes<WC, WP, TC, TP, S>() + 16 * TC * WC * 4 * (1 + WP)) * OCC <= 160 * 1024;
+}
 template <int WC, int WP, int TC, int TP, int S, int OCC>
 constexpr int block_smem_bytes() {
-  return block_ring_bytes<WC, WP, TC, TP, S>() + (block_lds_bias<WC, WP, TC, TP, S, OCC>() ? 16 * TC * WC * 4 : 0);
+  return block_ring_bytes<WC, WP, TC, TP, S>() + (block_lds_bias<WC, WP, TC, TP, S, OCC>() ? 16 * TC * WC * 4 : 0) +
+         (block_can_pool<WC, WP, TC, TP, S, OCC>() ? 16 * TC * WC * 4 * WP : 0);
 }
 
 template <typename T, int WC, int WP, int TC, int TP, int S, int OCC>
@@ -133,6 +141,7 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   // epilogues read it from LDS: a global load there would put a vmcnt wait on
   // whatever reuses its registers in the next K-step
   constexpr bool LDS_BIAS = block_lds_bias<WC, WP, TC, TP, S, OCC>();
+  constexpr bool POOL_OK = block_can_pool<WC, WP, TC, TP, S, OCC>();
   const float* s_bias = LDS_BIAS ? (const float*)(smem + S * STAGE) : a.bias + c0;
   if (LDS_BIAS && tid < BC / 4) *(float4*)(smem + S * STAGE + 16 * tid) = *(const float4*)(a.bias + c0 + 4 * tid);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
@@ -284,10 +293,44 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
       float4 bias[TC];
 #pragma unroll
       for (int i = 0; i < TC; ++i) bias[i] = *(const float4*)(s_bias + wc * 16 * TC + i * 16 + fg * 4);
+      if constexpr (POOL_OK) {
+        if (a.pool_out) {
+          // fused global average pool (the backbone's last conv; a tile = one
+          // image): relu(acc + bias) summed over the wave's pixels -- its TP
+          // fragments, then the 16 lanes of a row by DPP rotations -- then over
+          // the WP pixel waves through LDS, in a fixed order (deterministic)
+          float* s_pool = (float*)(smem + S * STAGE + BC * 4);
+#pragma unroll
+          for (int i = 0; i < TC; ++i) {
+            const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
+            float ps[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float v = 0.f;
+#pragma unroll
+              for (int j = 0; j < TP; ++j) v += fmaxf(acc[i][j][r] + bb[r], 0.f);
+              v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, true));
+              v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, true));
+              v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));
+              v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));
+              ps[r] = v;
+            }
+            if (fr == 0)
+              *(float4*)(s_pool + wp * BC + wc * 16 * TC + i * 16 + fg * 4) = make_float4(ps[0], ps[1], ps[2], ps[3]);
+          }
+          __syncthreads();
+          if (tid < BC) {
+            float sum = 0.f;
+#pragma unroll
+            for (int w2 = 0; w2 < WP; ++w2) sum += s_pool[w2 * BC + tid];
+            a.pool_out[(int64_t)ctile * a.Cout + c0 + tid] = sum * (1.f / BP);
+          }
+        }
+      }
 #pragma unroll
       for (int j = 0; j < TP; ++j) {
         const int px = ctile * BP + wp * 16 * TP + j * 16 + fr;
-        if (px < M) {
+        if (out != nullptr && px < M) {
 #pragma unroll
           for (int i = 0; i < TC; ++i) {
             const int co = c0 + wc * 16 * TC + i * 16 + fg * 4;
@@ -332,6 +375,11 @@ static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
   }
   constexpr int BC = 16 * TC * WC, BP = 16 * TP * WP;
   const int occupancy = OCC;
+  if (a.pool_out) {
+    SAD_REQUIRE((block_can_pool<WC, WP, TC, TP, S, OCC>()), "fused average pool: variant has no LDS for it");
+    SAD_REQUIRE(a.Ho * a.Wo == BP && a.M % BP == 0 && !a.res, "fused average pool: a pixel tile must be one image");
+  }
+  SAD_REQUIRE(a.out || a.pool_out, "null output");
   SAD_REQUIRE(a.Cout % BC == 0, "Cout must be a multiple of the channel tile");
   const int n_tc = a.Cout / BC;
   const int64_t tiles_p = (a.M + BP - 1) / BP;
@@ -395,6 +443,18 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
   if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo()))) return 20;
   return a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? 10 : 9);
+}
+// pixel tile of the variants that can fuse the average pool (0: cannot)
+static int pool_tile(int v) {
+  switch (v) {
+    case 13: case 14: case 15: return 256;
+    case 16: return 512;
+  }
+  return 0;
+}
+bool block_conv_can_pool(const BlockConvArgs& a, int dtype) {
+  const int bp = pool_tile(default_block_variant(a, dtype));
+  return bp > 0 && a.Ho * a.Wo == bp && !a.res && a.M % bp == 0;
 }
 static bool variant_fits(int v, int cout) {
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128};

@@ -42,6 +42,8 @@ struct BlockConvArgs {
   int64_t in0_bytes, in1_bytes, wt_bytes, res_bytes;  // set by launch_block_conv
   int ablate;            // timing ablations (wrong results): 1 no DMA in loop, 2 no vmcnt wait, 4 no barrier,
                          // 8 no epilogue, 16 no weight DMA, 32 no patch DMA (halo)
+  float* pool_out;       // optional fused global average pool, fp32 [N, Cout] (the variant's pixel tile
+                         // must be one image: block_conv_can_pool); out may then be null
 };
 
 struct StemArgs {
@@ -62,7 +64,8 @@ int default_conv_variant(const ConvArgs& a);
 int launch_stem(const StemArgs& a, int dtype, hipStream_t s);
 int launch_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, int variant = 0);
 int default_block_variant(const BlockConvArgs& a, int dtype);
-bool layer2_halo();  // SAD_L2_HALO (default 1): layer2's identity blocks on the halo kernel
+bool layer2_halo();
+bool block_conv_can_pool(const BlockConvArgs& a, int dtype);  // default variant pools Ho x Wo tiles  // SAD_L2_HALO (default 1): layer2's identity blocks on the halo kernel
 int launch_avgpool(const void* in, int64_t B, int hw, int c, float* out, int dtype, hipStream_t s);
 int launch_heads_final(const float* y2, int64_t B, int n_heads, const float* w3, const float* b3,
                        float* logits, float* merged, hipStream_t s);

@@ -176,3 +176,26 @@ def test_microbatch_invariance():
     a = Backbone(bases[0], DEV, 'bf16', micro_batch=16)(maps)
     b = Backbone(bases[0], DEV, 'bf16', micro_batch=37)(maps)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('dtype,tol', [('fp32', 1e-5), ('bf16', 4e-3)])
+def test_fused_avgpool_matches_separate_pool(dtype, tol):
+    """The last layer4 conv pools its relu(acc + bias) tiles itself (fused global
+    average pool, fp32 sums); the debug path stores the layer4 map (bf16 in the
+    throughput mode) and runs the separate avgpool kernel.  fp32: summation
+    order only; bf16: the stored map's rounding (2^-9 relative per element)."""
+    from sad.engine import Backbone, split_merged_state
+    from sad import _lib
+    _, bases, _ = split_merged_state(merged_sd('n6'))
+    fe_ = __import__('sad.engine', fromlist=['FrontEnd']).FrontEnd(DEV)
+    pcm = torch.empty(9, 128000, dtype=torch.int16, device=DEV)
+    _lib.call('sad_synth_pcm', 7, 0, 9, 128000, _lib.ptr(pcm), _lib.stream_handle(torch.device(DEV)))
+    maps = fe_(pcm)
+    bb = Backbone(bases[0], DEV, dtype, micro_batch=9)
+    fused = bb(maps)
+    sep, l4 = bb.debug(maps)
+    torch.cuda.synchronize()
+    ref = l4.float().mean(dim=(1, 2))
+    assert torch.allclose(sep, ref, rtol=1e-5, atol=1e-5)
+    err = ((fused - sep).abs().max() / sep.abs().max()).item()
+    assert err <= tol, err
