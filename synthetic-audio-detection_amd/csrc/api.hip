@@ -705,8 +705,19 @@ extern "C" int sad_heads_merge_run(const sad_heads_plan* p, const float* const* 
     if ((rc = launch_conv(a, SAD_F32, s))) return rc;
     col += 512 * G;
   }
-  for (int h = 0; h < N; ++h) {
+  // the N heads' Linear(512, 256) + BN1d + ReLU: one grouped launch when the
+  // heads' hidden columns are in head order (always for a shared backbone)
+  bool regular = true;
+  for (int h = 0; h < N; ++h) regular = regular && p->y1_col[h] == h * 512;
+  for (int h = 0; h < (regular ? 1 : N); ++h) {
     ConvArgs a{};
+    if (regular && N > 1) {
+      a.groups = N;
+      a.in_gstride = 512;
+      a.wt_gstride = (int64_t)256 * 512;
+      a.bias_gstride = 256;
+      a.out_gstride = 256;
+    }
     a.in = y1 + p->y1_col[h];
     a.in_pstride = (int64_t)N * 512;
     a.N = (int)B;

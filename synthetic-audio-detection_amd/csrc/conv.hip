@@ -53,6 +53,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_igemm_kernel(ConvArgs a)
   constexpr int NT = 64 * NW;               // threads
   constexpr int BM = 64 * WM, BN = 64 * WN;
   constexpr int ES = sizeof(T);
+  if (blockIdx.y > 0) {  // grouped launch: this group's operands (uniform)
+    const int g = blockIdx.y;
+    a.in = (const T*)a.in + g * a.in_gstride;
+    a.wt = (const T*)a.wt + g * a.wt_gstride;
+    a.bias = a.bias + g * a.bias_gstride;
+    a.out = (T*)a.out + g * a.out_gstride;
+  }
   constexpr int STAGE = (BM + BN) * 128;    // bytes per ring stage
   constexpr int QA = BM / 8 / NW;           // A LDS-DMA wave-instructions per wave per K-step
   constexpr int QB = BN / 8 / NW;           // B ...
@@ -684,7 +691,9 @@ static int launch_conv_t(const ConvArgs& a, hipStream_t s) {
   const int64_t tiles_m = (a.M + BM - 1) / BM;
   const int64_t nwg = tiles_m * (a.Cout / BN);
   SAD_REQUIRE(nwg < (1ll << 31), "grid too large");
-  hipLaunchKernelGGL((conv_igemm_kernel<T, WM, WN, S>), dim3((unsigned)nwg), dim3(64 * WM * WN), smem, s, a);
+  SAD_REQUIRE(a.groups <= 1 || !a.res, "grouped conv: no residual");
+  hipLaunchKernelGGL((conv_igemm_kernel<T, WM, WN, S>), dim3((unsigned)nwg, (unsigned)std::max(a.groups, 1)),
+                     dim3(64 * WM * WN), smem, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }

@@ -19,6 +19,11 @@ struct ConvArgs {
   int64_t M;             // N * Ho * Wo
   int64_t in_bytes;      // set by launch_conv: addressable input span (buffer range)
   int64_t wt_bytes;      // set by launch_conv
+  // optional grouped launch (grid.y = groups): group g reads in + g*in_gstride,
+  // wt + g*wt_gstride, bias + g*bias_gstride and writes out + g*out_gstride
+  // (elements) -- e.g. the N heads' Linear(512, 256) GEMMs as one launch
+  int groups;
+  int64_t in_gstride, wt_gstride, bias_gstride, out_gstride;
 };
 
 // One GEMM = 3x3 (or 1x1) conv of source 0 + optional 1x1 shortcut of source 1
