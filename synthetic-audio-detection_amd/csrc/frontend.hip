@@ -7,9 +7,10 @@
 // Kernel 1 (fe_mel_db): one workgroup = 4 waves = one segment x a block of 32
 //   STFT frames; each wave owns one frame at a time.  A 2048-point real frame
 //   is packed as a 1024-point complex sequence z[m] = y[2m] + i*y[2m+1] and
-//   transformed by a 5-pass radix-4 Stockham FFT whose butterflies run in
-//   registers and whose passes exchange through the wave's 8 KB LDS slot;
-//   twiddles (1024- and 2048-point, float64-accurate) live in LDS.  The real
+//   transformed by a four-step 16 x 64 FFT: 16-point DFTs in registers, ONE
+//   swizzled transpose through the wave's LDS slot, 16-point DFTs in registers
+//   plus a 4-point DFT across each lane quad (DPP); per-lane twiddles
+//   (float64-accurate table values) are held in registers for all frames.  The real
 //   spectrum is recovered for the bins the mel bank touches (2..768), powered,
 //   projected on the CSR mel bank (1515 nnz) and converted to dB.
 //   PCM reads: the first Stockham pass loads z straight from HBM, lane-
@@ -48,6 +49,41 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+// ---- four-step 1024-point FFT building blocks (one wave per frame) ----------
+// 4-point forward DFT in place: (x0, x1, x2, x3) -> (X0, X1, X2, X3)
+__device__ __forceinline__ void dft4(float2& a, float2& b, float2& c, float2& d) {
+  const float2 s02 = make_float2(a.x + c.x, a.y + c.y), d02 = make_float2(a.x - c.x, a.y - c.y);
+  const float2 s13 = make_float2(b.x + d.x, b.y + d.y), d13 = make_float2(b.x - d.x, b.y - d.y);
+  a = make_float2(s02.x + s13.x, s02.y + s13.y);
+  b = make_float2(d02.x + d13.y, d02.y - d13.x);  // x0 - i x1 - x2 + i x3
+  c = make_float2(s02.x - s13.x, s02.y - s13.y);
+  d = make_float2(d02.x - d13.y, d02.y + d13.x);  // x0 + i x1 - x2 - i x3
+}
+// W16^j = e^{-2 pi i j / 16}
+__device__ constexpr float W16R[10] = {1.f, 0.92387953251128674f, 0.70710678118654757f, 0.38268343236508978f, 0.f,
+                                       -0.38268343236508978f, -0.70710678118654757f, -0.92387953251128674f, -1.f,
+                                       -0.92387953251128674f};
+__device__ constexpr float W16I[10] = {0.f, -0.38268343236508978f, -0.70710678118654757f, -0.92387953251128674f, -1.f,
+                                       -0.92387953251128674f, -0.70710678118654757f, -0.38268343236508978f, 0.f,
+                                       0.38268343236508978f};
+// 16-point forward DFT in registers: t = 4 t1 + t2, k = k1 + 4 k2 (4-point DFTs
+// over t1, twiddles W16^{t2 k1}, 4-point DFTs over t2).  In: x[t]; out: X[k] at
+// x[fe_p16(k)].
+__device__ __forceinline__ constexpr int fe_p16(int k) { return 4 * (k & 3) + (k >> 2); }
+__device__ __forceinline__ void dft16(float2 (&x)[16]) {
+#pragma unroll
+  for (int t2 = 0; t2 < 4; ++t2) dft4(x[t2], x[4 + t2], x[8 + t2], x[12 + t2]);
+#pragma unroll
+  for (int k1 = 1; k1 < 4; ++k1)
+#pragma unroll
+    for (int t2 = 1; t2 < 4; ++t2) x[4 * k1 + t2] = cmul(x[4 * k1 + t2], make_float2(W16R[t2 * k1], W16I[t2 * k1]));
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) dft4(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3]);
+}
+// spectrum slot of bin k in the wave's buffer: 4 pad slots per 256 bins make the
+// final scatter (k = k1 + 16 k2a + 256 br(q)) bank-conflict-free
+__device__ __forceinline__ int fe_zslot(int k) { return k + 4 * (k >> 8); }
+
 // LDS exchange between the lanes of ONE wave: the wave's LDS operations
 // complete in order, so a compiler fence at wavefront scope is all that is
 // needed (no workgroup barrier: the four waves run independent frames).
@@ -58,10 +94,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 constexpr int FE_STAGE_MELS = 128;  // dB rows staged in LDS for coalesced stores
-constexpr int FE_POW = FE_NC + 4;   // power bins per wave in LDS (any bin range of the 1025)
+constexpr int FE_POW = 800;         // power bins per wave in LDS (the reference's bank: 767)
+constexpr int FE_ZBUF = FE_NC + 16;  // spectrum slots per wave (fe_zslot padding)
 constexpr int FE_MAX_NNZ = 1600;    // mel weights in LDS (1515 for the reference's bank)
-// LDS: twiddles 8 KB + 4 FFT buffers 32 KB + power 16 KB + dB staging 16.5 KB +
-// mel weights 6.3 KB = 79 KB: two workgroups per CU.
+// LDS: twiddles 8 KB + 4 FFT buffers 32.5 KB + power 12.5 KB + dB staging 16.5 KB +
+// mel weights 6.3 KB = 76 KB: two workgroups per CU.
 
 template <typename IT>  // int16_t PCM (scaled by 1/32768, torchaudio.load normalize) or float
 __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
@@ -70,7 +107,8 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     const int* __restrict__ mel_len, const int* __restrict__ mel_off, const float* __restrict__ mel_w, int nnz,
     int n_mels, int bin_lo, int bin_hi, float* __restrict__ out) {
   __shared__ float2 s_tw[FE_NC];
-  __shared__ float2 s_buf[FE_WAVES][FE_NC];
+  __shared__ float2 s_buf[FE_WAVES][FE_ZBUF];
+  __shared__ float2 s_tw3[64];  // W64^{q k2} at [k2][q]
   __shared__ float s_pow[FE_WAVES][FE_POW];
   __shared__ float s_db[FE_STAGE_MELS][FE_FRAMES_PER_WG + 1];
   __shared__ float s_melw[FE_MAX_NNZ];
@@ -97,6 +135,16 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
   }
   __syncthreads();
 
+  // step 2's per-lane twiddles W1024^{l k1} (l = lane) in registers for all
+  // frames; step 3's W64^{q k2} (q = lane & 3) as a [k2][q] LDS table
+  float2 tw2[16];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) tw2[k] = s_tw[(lane * k) & (FE_NC - 1)];
+  if (tid < 64) s_tw3[tid] = s_tw[(16 * (tid & 3) * (tid >> 2)) & (FE_NC - 1)];  // [k2][q]
+  __syncthreads();
+  const int fg4 = lane >> 2, fq = lane & 3;
+  const int fbr = (fq == 1 ? 2 : fq == 2 ? 1 : fq);  // bit-reversed q (output block of the lane)
+
   const int f_begin = blockIdx.x * FE_FRAMES_PER_WG;
   const int f_end = min(n_frames, f_begin + FE_FRAMES_PER_WG);
   float2* buf = s_buf[wave];
@@ -106,7 +154,7 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
   const bool pairs = ((hop & 1) == 0) && ((seg_stride & 1) == 0) && ((((uintptr_t)pcm) & (2 * sizeof(IT) - 1)) == 0);
 
   for (int t = f_begin + wave; t < f_end; t += FE_WAVES) {
-    float2 v[4][4];
+    float2 x16[16];  // z[lane + 64 t'], t' = b + 4 r
     // ---- pass 0 input: z[m] = (y[2m], y[2m+1]) windowed, m = j + 256 r; one
     // 2-sample load per lane (coalesced) where the frame needs no reflection
     const int base = t * hop - pad;
@@ -138,50 +186,45 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
           e1 = (float)x[i1];
         }
         const float2 wv = *(const float2*)(window + 2 * m);
-        v[b][r] = make_float2(e0 * in_scale * wv.x, e1 * in_scale * wv.y);
+        x16[b + 4 * r] = make_float2(e0 * in_scale * wv.x, e1 * in_scale * wv.y);
       }
     }
-    // ---- 5 radix-4 Stockham passes, Ns = 1, 4, 16, 64, 256 (wave-local)
+    // ---- four-step FFT, N = 16 x 64: Z[k1 + 16 k2] = sum_l W64^{l k2} W1024^{l k1}
+    // sum_t z[l + 64 t] W16^{t k1}.  Step 1 (16-point DFT over t) and its twiddle
+    // in registers; ONE LDS transpose (XOR-swizzled: conflict-free both ways);
+    // step 3's 64-point DFTs as 4 lanes x 16 registers: a 16-point DFT in
+    // registers, twiddle, then a 4-point DFT across the lanes of a quad (DPP).
+    dft16(x16);
 #pragma unroll
-    for (int p = 0; p < 5; ++p) {
-      const int Ns = 1 << (2 * p);
-      if (p > 0) {
-        wave_lds_sync();
+    for (int k1 = 1; k1 < 16; ++k1) x16[fe_p16(k1)] = cmul(x16[fe_p16(k1)], tw2[k1]);
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int j = lane + 64 * b;
+    for (int k1 = 0; k1 < 16; ++k1) buf[k1 * 64 + (lane ^ (4 * k1))] = x16[fe_p16(k1)];
+    wave_lds_sync();
+    // lane (g, q) = (lane >> 2, lane & 3): B[l = q + 4 s][k1 = g], s = 0..15
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[b][r] = buf[j + 256 * r];
-        }
-        wave_lds_sync();
-      }
+    for (int s2 = 0; s2 < 16; ++s2) x16[s2] = buf[fg4 * 64 + ((fq + 4 * s2) ^ (4 * fg4))];
+    wave_lds_sync();
+    dft16(x16);
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int j = lane + 64 * b;
-        const int k = j & (Ns - 1);
-        if (p > 0) {
-          const int tstep = FE_NC / (Ns * 4);  // angle index step per r
-#pragma unroll
-          for (int r = 1; r < 4; ++r) v[b][r] = cmul(v[b][r], s_tw[(k * r * tstep) & (FE_NC - 1)]);
-        }
-        // radix-4 forward DFT
-        const float2 a0 = v[b][0], a1 = v[b][1], a2 = v[b][2], a3 = v[b][3];
-        const float2 s02 = make_float2(a0.x + a2.x, a0.y + a2.y);
-        const float2 d02 = make_float2(a0.x - a2.x, a0.y - a2.y);
-        const float2 s13 = make_float2(a1.x + a3.x, a1.y + a3.y);
-        const float2 d13 = make_float2(a1.x - a3.x, a1.y - a3.y);
-        const int idxD = (j / Ns) * Ns * 4 + k;
-        buf[idxD] = make_float2(s02.x + s13.x, s02.y + s13.y);
-        buf[idxD + Ns] = make_float2(d02.x + d13.y, d02.y - d13.x);      // a0 - i a1 - a2 + i a3
-        buf[idxD + 2 * Ns] = make_float2(s02.x - s13.x, s02.y - s13.y);
-        buf[idxD + 3 * Ns] = make_float2(d02.x - d13.y, d02.y + d13.x);  // a0 + i a1 - a2 - i a3
-      }
+    for (int k2 = 0; k2 < 16; ++k2) {
+      float2 d = x16[fe_p16(k2)];
+      if (k2 > 0) d = cmul(d, s_tw3[4 * k2 + fq]);
+      // 4-point DFT over q across the quad: radix-2 stages with partners q^2, q^1
+      const float px = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d.x), 0x4E, 0xF, 0xF, true));
+      const float py = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d.y), 0x4E, 0xF, 0xF, true));
+      float2 u = fq < 2 ? make_float2(d.x + px, d.y + py) : make_float2(px - d.x, py - d.y);
+      if (fq == 3) u = make_float2(u.y, -u.x);  // x W4^1 = -i
+      const float qx = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(u.x), 0xB1, 0xF, 0xF, true));
+      const float qy = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(u.y), 0xB1, 0xF, 0xF, true));
+      // lane (g, q) holds Z[g + 16 k2 + 256 br(q)]
+      buf[fe_zslot(fg4 + 16 * k2 + 256 * fbr)] =
+          (fq & 1) == 0 ? make_float2(u.x + qx, u.y + qy) : make_float2(qx - u.x, qy - u.y);
     }
     wave_lds_sync();
     // ---- real-spectrum recovery + power for bins [bin_lo, bin_hi]
     for (int k = bin_lo + lane; k <= bin_hi; k += 64) {
-      const float2 A = buf[k & (FE_NC - 1)];
-      const float2 Bc = buf[(FE_NC - k) & (FE_NC - 1)];
+      const float2 A = buf[fe_zslot(k & (FE_NC - 1))];
+      const float2 Bc = buf[fe_zslot((FE_NC - k) & (FE_NC - 1))];
       const float2 B = make_float2(Bc.x, -Bc.y);              // conj(Z[N/2-k])
       const float2 E = make_float2(0.5f * (A.x + B.x), 0.5f * (A.y + B.y));
       const float2 D = make_float2(A.x - B.x, A.y - B.y);
