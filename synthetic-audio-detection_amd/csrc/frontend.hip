@@ -13,7 +13,7 @@
 //   (float64-accurate table values) are held in registers for all frames.  The real
 //   spectrum is recovered for the bins the mel bank touches (2..768), powered,
 //   projected on the CSR mel bank (1515 nnz) and converted to dB.
-//   PCM reads: the first Stockham pass loads z straight from HBM, lane-
+//   PCM reads: the FFT input z is loaded straight from HBM, lane-
 //   consecutive int16 pairs (coalesced); reflect padding is index arithmetic.
 // Kernel 2 (fe_normalize): one workgroup per segment: max -> top-db clamp ->
 //   float64 mean / unbiased variance -> standardise (32,128 values).
