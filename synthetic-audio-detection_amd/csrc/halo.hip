@@ -540,10 +540,10 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
       constexpr int k = decltype(kc)::value;
       __builtin_amdgcn_sched_barrier(0);
       // next tile's patch: one piece per tap over taps 0..QP-1; this tile's
-      // residual: fragment j at tap 1 + j
+      // residual: fragment j at tap j
       if constexpr (k < QP)
         if (has_next) patch_piece(k, pb ^ 1);
-      if constexpr (k >= 1 && k <= TP) load_res(t, k - 1);
+      if constexpr (k < TP) load_res(t, k);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (k < 8) {
         read_tap(wf[(k + 1) & 1], pf[(k + 1) & 1], k + 1, pb);
