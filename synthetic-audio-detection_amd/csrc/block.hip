@@ -439,10 +439,21 @@ bool layer2_halo() {
   }();
   return v;
 }
+// SAD_C128_VARIANT: block-conv variant for Cout = 128 GEMM convs (layer2's first
+// block; A/B switch).  15 (128x256, 8 waves, 3 stages) over 10 (128x128, 4
+// waves, 2 workgroups/CU): l2.c1 580 -> 473 us in isolation at mb 512, +0.5 %
+// end-to-end same-box (gpurun_out/ab_c128.log)
+static int c128_variant() {
+  static const int v = [] {
+    const char* e = getenv("SAD_C128_VARIANT");
+    return e ? atoi(e) : 15;
+  }();
+  return v;
+}
 int default_block_variant(const BlockConvArgs& a, int dtype) {
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
   if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo()))) return 20;
-  return a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? 10 : 9);
+  return a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9);
 }
 // pixel tile of the variants that can fuse the average pool (0: cannot)
 static int pool_tile(int v) {

@@ -111,7 +111,8 @@ def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,)):
         Ho = H // s
         cin0 = Cin if sc is None else Cout
         h0 = H if sc is None else Ho
-        K = 9 * cin0 + (0 if sc is None else (Cout if sc == 'id' else Cin))
+        cin1 = Cout // 2  # the downsample reads the previous stage's map (Cout/2 channels, 2x the side)
+        K = 9 * cin0 + (0 if sc is None else (Cout if sc == 'id' else cin1))
         w = (torch.randn(Cout, K, device=dev) * (1.0 / K) ** 0.5).to(torch.bfloat16)
         bias = torch.randn(Cout, device=dev) * 0.1
         for mb in mbs:
@@ -120,7 +121,7 @@ def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,)):
             if sc == 'id':
                 scx = torch.randn(mb, Ho, Ho, Cout, device=dev).to(torch.bfloat16)
             elif sc == 'ds':
-                scx = torch.randn(mb, 2 * Ho, 2 * Ho, Cin, device=dev).to(torch.bfloat16)
+                scx = torch.randn(mb, 2 * Ho, 2 * Ho, cin1, device=dev).to(torch.bfloat16)
             stride = s if sc is None else 1
             flop = 2.0 * mb * Ho * Ho * Cout * K
             ref = None
