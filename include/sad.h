@@ -134,6 +134,36 @@ int sad_backbone_run_debug(const sad_backbone_plan* plan, const float* map, int6
                            float* feats, void* layer4_out, void* workspace, size_t ws_bytes,
                            void* stream);
 
+/* Deeper timm ResNets (resnet34/50/101/152, the
+ * `--model-name` choices of submodel_trainer.py:51 / model_merger.py:24 /
+ * inference_runner.py:77 backbone_name), on the same kernels: fused
+ * resize+stem, block-conv GEMMs (downsample folded into the block's last GEMM
+ * as extra K columns), the implicit-GEMM conv for Bottleneck identity adds,
+ * then the average pool.  Replaces timm.create_model(name, num_classes=0)
+ * .forward_features + global pool:  map -> pooled [B, num_features] fp32.
+ * block: SAD_BASIC_BLOCK (resnet18/34: conv1/bn1, conv2/bn2 per block) or
+ * SAD_BOTTLENECK (resnet50/101/152: conv1/bn1, conv2/bn2, conv3/bn3, width =
+ * planes, expansion 4, stride on conv2 as timm).  layers: blocks per stage
+ * ([3,4,6,3] for resnet34/50).  params: 5 pointers per conv+BN in timm
+ * state-dict order (conv1/bn1 first; per block its convs, then
+ * downsample.0/downsample.1 where present). */
+#define SAD_BASIC_BLOCK 0
+#define SAD_BOTTLENECK 1
+typedef struct sad_resnet_plan sad_resnet_plan;
+int sad_resnet_plan_create(const float* const* params, int32_t n_params, int32_t block,
+                           const int32_t* layers, int32_t dtype, int32_t map_h, int32_t map_w,
+                           sad_resnet_plan** out);
+int sad_resnet_plan_destroy(sad_resnet_plan* plan);
+/* pooled feature width: 512 (BasicBlock) or 2048 (Bottleneck) */
+int sad_resnet_num_features(const sad_resnet_plan* plan, int32_t* n);
+int sad_resnet_workspace_size(const sad_resnet_plan* plan, int64_t micro_batch, size_t* bytes);
+/* map: [B, map_h, map_w] fp32; feats: [B, num_features] fp32 */
+int sad_resnet_run(const sad_resnet_plan* plan, const float* map, int64_t B, int64_t micro_batch,
+                   float* feats, void* workspace, size_t ws_bytes, void* stream);
+/* same from resized images img [B, 512, 512] fp32 (one of the 3 identical channels) */
+int sad_resnet_run_img(const sad_resnet_plan* plan, const float* img, int64_t B, int64_t micro_batch,
+                       float* feats, void* workspace, size_t ws_bytes, void* stream);
+
 /* Kernel-level timing of the backbone's block-conv launches (bench.py's
  * roofline of the dominant kernel): between begin and end, every block-conv
  * launch of sad_backbone_run* is bracketed by HIP events on its stream.  end()
@@ -156,6 +186,11 @@ typedef struct sad_heads_plan sad_heads_plan;
 
 int sad_heads_plan_create(const float* const* params, int32_t n_heads, const int32_t* feat_index,
                           int32_t n_feat, sad_heads_plan** out);
+/* Same with the backbone feature width feat_dim (2.weight is [512, feat_dim];
+ * 2048 for Bottleneck ResNets, whose head is Linear(2048, 512),
+ * inference_runner.py:39 with base.num_features); feats are [B, feat_dim]. */
+int sad_heads_plan_create_dim(const float* const* params, int32_t n_heads, const int32_t* feat_index,
+                              int32_t n_feat, int32_t feat_dim, sad_heads_plan** out);
 int sad_heads_plan_destroy(sad_heads_plan* plan);
 int sad_heads_workspace_size(const sad_heads_plan* plan, int64_t B, size_t* bytes);
 /* feats: n_feat pointers to [B,512] fp32; logits: [B, N, 2] fp32 (per head

@@ -4,7 +4,9 @@ TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
 
 * ``ResNet`` restates ``timm.create_model('resnet18', num_classes=0)`` as called
   at ``inference_runner.py:35`` / ``model_merger.py:24`` /
-  ``submodel_trainer.py:606``: BasicBlock ResNet, conv1 7x7/2 + bn1 + act1 +
+  ``submodel_trainer.py:606`` (and the deeper names those call sites accept:
+  resnet34 BasicBlocks; resnet50/101/152 Bottlenecks, timm's v1.5 layout with
+  the stride on the 3x3 conv): BasicBlock ResNet, conv1 7x7/2 + bn1 + act1 +
   maxpool 3x3/2, layer1..4, 1x1/2 conv + BN downsample; ``forward_features``
   returns the layer4 map.  Parameter/buffer names match timm's state-dict keys
    so reference checkpoints load unchanged.
@@ -44,10 +46,37 @@ class BasicBlock(nn.Module):
         return self.act2(x)
 
 
-class ResNet(nn.Module):
-    """timm ResNet with BasicBlocks; ``layers`` = [2,2,2,2] is resnet18."""
+class Bottleneck(nn.Module):
+    """timm Bottleneck (resnet50/101/152): 1x1 -> 3x3/s -> 1x1 (x4), width = planes."""
+    expansion = 4
 
-    def __init__(self, layers=(2, 2, 2, 2), in_chans: int = 3):
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.act1 = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.act2 = nn.ReLU(inplace=True)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.act3 = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        shortcut = x
+        x = self.act1(self.bn1(self.conv1(x)))
+        x = self.act2(self.bn2(self.conv2(x)))
+        x = self.bn3(self.conv3(x))
+        if self.downsample is not None:
+            shortcut = self.downsample(shortcut)
+        return self.act3(x + shortcut)
+
+
+class ResNet(nn.Module):
+    """timm ResNet; ``layers`` = [2,2,2,2] with BasicBlocks is resnet18."""
+
+    def __init__(self, layers=(2, 2, 2, 2), in_chans: int = 3, block=BasicBlock):
         super().__init__()
         self.conv1 = nn.Conv2d(in_chans, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = nn.BatchNorm2d(64)
@@ -60,13 +89,13 @@ class ResNet(nn.Module):
             for b in range(n):
                 s = stride if b == 0 else 1
                 ds = None
-                if b == 0 and (s != 1 or inplanes != planes):
-                    ds = nn.Sequential(nn.Conv2d(inplanes, planes, 1, stride=s, bias=False),
-                                       nn.BatchNorm2d(planes))
-                blocks.append(BasicBlock(inplanes, planes, s, ds))
-                inplanes = planes
+                if b == 0 and (s != 1 or inplanes != planes * block.expansion):
+                    ds = nn.Sequential(nn.Conv2d(inplanes, planes * block.expansion, 1, stride=s, bias=False),
+                                       nn.BatchNorm2d(planes * block.expansion))
+                blocks.append(block(inplanes, planes, s, ds))
+                inplanes = planes * block.expansion
             self.add_module(f'layer{i + 1}', nn.Sequential(*blocks))
-        self.num_features = 512
+        self.num_features = 512 * block.expansion
         # timm: global_pool + fc(Identity) for num_classes=0 -> no parameters.
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
@@ -88,11 +117,14 @@ class ResNet(nn.Module):
 def create_model(model_name: str = 'resnet18', pretrained: bool = False, num_classes: int = 0, **kw):
     """Offline stand-in for ``timm.create_model`` (pretrained weights are a network
     fetch and unavailable here)."""
-    depths = {'resnet18': (2, 2, 2, 2), 'resnet34': (3, 4, 6, 3)}
+    depths = {'resnet18': (BasicBlock, (2, 2, 2, 2)), 'resnet34': (BasicBlock, (3, 4, 6, 3)),
+              'resnet50': (Bottleneck, (3, 4, 6, 3)), 'resnet101': (Bottleneck, (3, 4, 23, 3)),
+              'resnet152': (Bottleneck, (3, 8, 36, 3))}
     if model_name not in depths:
-        raise ValueError(f'unsupported backbone {model_name!r} (BasicBlock ResNets only)')
+        raise ValueError(f'unsupported backbone {model_name!r}')
     assert num_classes == 0
-    return ResNet(depths[model_name])
+    block, layers = depths[model_name]
+    return ResNet(layers, block=block)
 
 
 def make_head(num_features: int = 512) -> nn.Sequential:

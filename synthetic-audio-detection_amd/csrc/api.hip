@@ -69,6 +69,7 @@ struct sad_backbone_plan {
 
 struct sad_heads_plan {
   int n_heads, n_feat;
+  int feat_dim;                    // backbone feature width (512: ResNet-18/34; 2048: Bottleneck ResNets)
   int device;
   std::vector<int> feat_index;
   std::vector<int> group_of;      // head -> group (== feat index order of appearance)
@@ -94,8 +95,9 @@ extern "C" int sad_init(int device) {
 }
 
 // ------------------------------------------------------------- folding ----
-static void fold_bn(const float* g, const float* beta, const float* mu, const float* var, int c,
-                    std::vector<double>& scale, std::vector<double>& shift) {
+namespace sad {
+void fold_bn(const float* g, const float* beta, const float* mu, const float* var, int c,
+             std::vector<double>& scale, std::vector<double>& shift) {
   scale.resize(c);
   shift.resize(c);
   for (int i = 0; i < c; ++i) {
@@ -104,14 +106,7 @@ static void fold_bn(const float* g, const float* beta, const float* mu, const fl
   }
 }
 
-template <typename V>
-static int upload(void** dst, const std::vector<V>& v) {
-  SAD_CHECK_HIP(hipMalloc(dst, v.size() * sizeof(V)));
-  SAD_CHECK_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(V), hipMemcpyHostToDevice));
-  return SAD_OK;
-}
-
-static int upload_typed(void** dst, const std::vector<double>& v, int dtype) {
+int upload_typed(void** dst, const std::vector<double>& v, int dtype) {
   if (dtype == SAD_BF16) {
     std::vector<u16> h(v.size());
     for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_host((float)v[i]);
@@ -121,6 +116,30 @@ static int upload_typed(void** dst, const std::vector<double>& v, int dtype) {
   for (size_t i = 0; i < v.size(); ++i) h[i] = (float)v[i];
   return upload(dst, h);
 }
+
+// conv1 7x7/2 + bn1 folded for the stem kernel, the 3 identical input channels
+// summed; k = ky*7+kx padded to 64 (params: conv weight, BN weight/bias/mean/var)
+int fold_stem(const float* const* params, int dtype, void** w_out, float** b_out) {
+  const float* W = params[0];
+  std::vector<double> sc, sh;
+  fold_bn(params[1], params[2], params[3], params[4], 64, sc, sh);
+  std::vector<double> w(64 * 64, 0.0);
+  std::vector<float> b(64);
+  for (int co = 0; co < 64; ++co) {
+    for (int k = 0; k < 49; ++k) {
+      double s = 0.0;
+      for (int c = 0; c < 3; ++c) s += (double)W[(co * 3 + c) * 49 + k];
+      // bf16 stem: (ky, kx) on an 8x8 grid; f32 stem: k = ky*7+kx, k=4q+g at g*16+q
+      const int pos = dtype == SAD_BF16 ? (k / 7) * 8 + (k % 7) : ((k & 3) * 16 + (k >> 2));
+      w[co * 64 + pos] = s * sc[co];
+    }
+    b[co] = (float)sh[co];
+  }
+  int rc;
+  if ((rc = upload_typed(w_out, w, dtype))) return rc;
+  return upload((void**)b_out, b);
+}
+}  // namespace sad
 
 extern "C" int sad_backbone_plan_create(const float* const* params, int32_t n_params, int32_t dtype,
                                         int32_t map_h, int32_t map_w, sad_backbone_plan** out) {
@@ -137,25 +156,7 @@ extern "C" int sad_backbone_plan_create(const float* const* params, int32_t n_pa
   (void)hipGetDevice(&p->device);
   std::vector<double> sc, sh;
   int rc;
-  // stem: fold BN and the 3 identical input channels; k = ky*7+kx padded to 64
-  {
-    const float* W = params[0];
-    fold_bn(params[1], params[2], params[3], params[4], 64, sc, sh);
-    std::vector<double> w(64 * 64, 0.0), b(64);
-    for (int co = 0; co < 64; ++co) {
-      for (int k = 0; k < 49; ++k) {
-        double s = 0.0;
-        for (int c = 0; c < 3; ++c) s += (double)W[(co * 3 + c) * 49 + k];
-        // bf16 stem: (ky, kx) on an 8x8 grid; f32 stem: k = ky*7+kx, k=4q+g at g*16+q
-        const int pos = dtype == SAD_BF16 ? (k / 7) * 8 + (k % 7) : ((k & 3) * 16 + (k >> 2));
-        w[co * 64 + pos] = s * sc[co];
-      }
-      b[co] = sh[co];
-    }
-    if ((rc = upload_typed(&p->stem_w, w, dtype))) return rc;
-    std::vector<float> bf(b.begin(), b.end());
-    if ((rc = upload((void**)&p->stem_b, bf))) return rc;
-  }
+  if ((rc = fold_stem(params, dtype, &p->stem_w, &p->stem_b))) return rc;
   for (size_t ci = 1; ci < specs.size(); ++ci) {
     const ConvSpec& s = specs[ci];
     const float* W = params[ci * 5];
@@ -591,11 +592,19 @@ extern "C" int sad_backbone_run_img(const sad_backbone_plan* p, const float* img
 // ---------------------------------------------------------------- heads ----
 extern "C" int sad_heads_plan_create(const float* const* params, int32_t n_heads, const int32_t* feat_index,
                                      int32_t n_feat, sad_heads_plan** out) {
+  return sad_heads_plan_create_dim(params, n_heads, feat_index, n_feat, 512, out);
+}
+
+extern "C" int sad_heads_plan_create_dim(const float* const* params, int32_t n_heads, const int32_t* feat_index,
+                                         int32_t n_feat, int32_t feat_dim, sad_heads_plan** out) {
   SAD_REQUIRE(params && out && n_heads > 0 && n_feat > 0, "bad args");
+  SAD_REQUIRE(feat_dim > 0 && feat_dim % 64 == 0, "feat_dim must be a positive multiple of 64");
   for (int i = 0; i < n_heads * 14; ++i) SAD_REQUIRE(params[i], "null head parameter");
   auto* p = new sad_heads_plan();
   p->n_heads = n_heads;
   p->n_feat = n_feat;
+  p->feat_dim = feat_dim;
+  const int D = feat_dim;
   (void)hipGetDevice(&p->device);
   p->groups.assign(n_feat, {});
   for (int h = 0; h < n_heads; ++h) {
@@ -609,12 +618,13 @@ extern "C" int sad_heads_plan_create(const float* const* params, int32_t n_heads
   std::vector<double> sc, sh;
   for (int f = 0; f < n_feat; ++f) {
     const auto& g = p->groups[f];
-    std::vector<float> w1((size_t)g.size() * 512 * 512), b1(g.size() * 512);
+    std::vector<float> w1((size_t)g.size() * 512 * D), b1(g.size() * 512);
     for (size_t gi = 0; gi < g.size(); ++gi) {
       const float* const* hp = params + g[gi] * 14;
       fold_bn(hp[2], hp[3], hp[4], hp[5], 512, sc, sh);
       for (int o = 0; o < 512; ++o) {
-        for (int i = 0; i < 512; ++i) w1[(gi * 512 + o) * 512 + i] = (float)((double)hp[0][o * 512 + i] * sc[o]);
+        for (int i = 0; i < D; ++i)
+          w1[(gi * 512 + o) * D + i] = (float)((double)hp[0][(size_t)o * D + i] * sc[o]);
         b1[gi * 512 + o] = (float)((double)hp[1][o] * sc[o] + sh[o]);
       }
       p->y1_col[g[gi]] = col;
@@ -687,10 +697,10 @@ extern "C" int sad_heads_merge_run(const sad_heads_plan* p, const float* const* 
     SAD_REQUIRE(feats[f], "null feature pointer");
     ConvArgs a{};
     a.in = feats[f];
-    a.in_pstride = 512;
+    a.in_pstride = p->feat_dim;
     a.N = (int)B;
     a.H = a.W = 1;
-    a.Cin = 512;
+    a.Cin = p->feat_dim;
     a.wt = p->w1[f];
     a.bias = p->b1[f];
     a.out = y1 + col;

@@ -1,5 +1,7 @@
 // kernels.hpp -- launch interfaces shared by the kernel translation units.
 #pragma once
+#include <vector>
+
 #include "common.hpp"
 
 namespace sad {
@@ -74,5 +76,19 @@ bool block_conv_can_pool(const BlockConvArgs& a, int dtype);  // default variant
 int launch_avgpool(const void* in, int64_t B, int hw, int c, float* out, int dtype, hipStream_t s);
 int launch_heads_final(const float* y2, int64_t B, int n_heads, const float* w3, const float* b3,
                        float* logits, float* merged, hipStream_t s);
+
+// ---- host-side plan helpers (api.hip)
+template <typename V>
+int upload(void** dst, const std::vector<V>& v) {
+  SAD_CHECK_HIP(hipMalloc(dst, v.size() * sizeof(V)));
+  SAD_CHECK_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(V), hipMemcpyHostToDevice));
+  return SAD_OK;
+}
+// BN (eval) as a per-channel affine: scale = g / sqrt(var + 1e-5), shift = beta - mu * scale
+void fold_bn(const float* g, const float* beta, const float* mu, const float* var, int c,
+             std::vector<double>& scale, std::vector<double>& shift);
+int upload_typed(void** dst, const std::vector<double>& v, int dtype);  // fp32 or bf16 (RNE)
+// timm conv1 + bn1 (5 arrays) -> the stem kernel's weight layout and bias
+int fold_stem(const float* const* params, int dtype, void** w_out, float** b_out);
 
 }  // namespace sad

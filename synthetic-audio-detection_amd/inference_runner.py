@@ -58,13 +58,14 @@ class BinaryClassifier:
         """init='random': deterministic random backbone/head (stand-in for the
         reference's timm ``pretrained=True`` ImageNet weights, a network
         download); init='empty': shapes only, for loading a checkpoint."""
-        if model_name != 'resnet18':
-            raise ValueError(f'only resnet18 backbones are supported on the device path (got {model_name!r})')
+        # resnet18 (the reference's only inference backbone, :77,246) runs on the
+        # tuned plan; resnet34/50/101/152 on the generic ResNet plan (ValueError otherwise)
+        nf = _weights.arch_spec(model_name)[2]
         self.model_name = model_name
         if init == 'random':
-            bb, hd = _weights.backbone_state_dict(seed), _weights.head_state_dict(seed)
+            bb, hd = _weights.backbone_state_dict(seed, model_name), _weights.head_state_dict(seed, nf)
         else:
-            bb, hd = _weights.empty_state_dicts()
+            bb, hd = _weights.empty_state_dicts(model_name)
         sd = OrderedDict()
         for k, v in bb.items():
             sd[f'base.{k}'] = v

@@ -7,6 +7,8 @@ This is the MI355X replacement of the reference's device work:
   * ``Backbone``  -- timm resnet18 forward_features + AdaptiveAvgPool2d
     (inference_runner.py:35,37,49-51), with Resize((512,512)) + repeat(3)
     (:172-174) fused into the stem
+  * ``ResNetBackbone`` -- the deeper timm names (resnet34/50/101/152,
+    SURVEY.md 8(f) row 4) on the same kernels (libsad sad_resnet_*)
   * ``Heads``     -- BinaryClassifier.head x N + ModularMultiHeadClassifier
     merge (inference_runner.py:36-48,62-73)
   * ``Engine``    -- a merged checkpoint's state dict -> the three above.
@@ -24,7 +26,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .weights import backbone_param_shapes
+from .weights import arch_of_state, arch_param_shapes, arch_spec, backbone_param_shapes
 
 MAP_H, MAP_W = 128, 251
 N_SAMPLES = 128000
@@ -175,12 +177,72 @@ class Backbone:
             pass
 
 
+class ResNetBackbone:
+    """A timm resnet34/50/101/152 backbone (``base_sd`` in timm keys) on the
+    generic libsad ResNet plan: map -> pooled [B, num_features] fp32."""
+
+    def __init__(self, base_sd: Dict[str, torch.Tensor], model_name: str, device='cuda', dtype: str = 'bf16',
+                 micro_batch: int = 64):
+        self.device = _dev(device)
+        self.dtype = dtype
+        self.model_name = model_name
+        block, layers, self.num_features = arch_spec(model_name)
+        self._dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
+        # the widest activation (layer1 of a Bottleneck net: 128x128x256) must
+        # stay under the kernels' 2 GiB buffer-addressing range
+        self.micro_batch = max(1, min(micro_batch, 64))
+        arrays = []
+        for key, _shape, kind in arch_param_shapes(model_name):
+            if kind == 'conv':
+                arrays.append(_np32(base_sd[f'{key}.weight']))
+            else:
+                for s in ('weight', 'bias', 'running_mean', 'running_var'):
+                    arrays.append(_np32(base_sd[f'{key}.{s}']))
+        self._keep = arrays
+        lay = (_lib.I32 * 4)(*layers)
+        self._plan = _lib.P()
+        with torch.cuda.device(self.device):
+            _lib.call('sad_resnet_plan_create', _lib.pointer_array(arrays), len(arrays),
+                      1 if block == 'bottleneck' else 0, lay, self._dt, MAP_H, MAP_W, _lib.ctypes.byref(self._plan))
+        self._ws = None
+
+    def _run(self, fn: str, x: torch.Tensor, out: torch.Tensor | None) -> torch.Tensor:
+        B = x.shape[0]
+        feats = out if out is not None else torch.empty(B, self.num_features, device=self.device,
+                                                        dtype=torch.float32)
+        mb = max(1, min(self.micro_batch, B))
+        sz = _lib.SZ()
+        _lib.call('sad_resnet_workspace_size', self._plan, mb, _lib.ctypes.byref(sz))
+        if self._ws is None or self._ws.numel() < sz.value:
+            self._ws = torch.empty(sz.value, dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.call(fn, self._plan, _lib.ptr(x), B, mb, _lib.ptr(feats), _lib.ptr(self._ws),
+                      self._ws.numel(), _lib.stream_handle(self.device))
+        return feats
+
+    def __call__(self, maps: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        assert maps.dtype == torch.float32 and maps.shape[1:] == (MAP_H, MAP_W) and maps.is_contiguous()
+        return self._run('sad_resnet_run', maps, out)
+
+    def forward_images(self, img: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """img [B,512,512] fp32 (one channel of the reference's identical three) -> feats."""
+        assert img.dtype == torch.float32 and img.shape[1:] == (512, 512) and img.is_contiguous()
+        return self._run('sad_resnet_run_img', img, out)
+
+    def __del__(self):
+        try:
+            if getattr(self, '_plan', None):
+                _lib.load().sad_resnet_plan_destroy(self._plan)
+        except Exception:
+            pass
+
+
 class Heads:
     """N BinaryClassifier heads (+ merge); ``head_sds[h]`` uses nn.Sequential
     index keys (2.weight, 3.running_mean, ...)."""
 
     def __init__(self, head_sds: Sequence[Dict[str, torch.Tensor]], feat_index: Sequence[int], n_feat: int,
-                 device='cuda'):
+                 device='cuda', feat_dim: int = 512):
         self.device = _dev(device)
         self.n_heads = len(head_sds)
         arrays = [_np32(sd[k]) for sd in head_sds for k in HEAD_KEYS]
@@ -188,8 +250,8 @@ class Heads:
         fi = (_lib.I32 * self.n_heads)(*feat_index)
         self._plan = _lib.P()
         with torch.cuda.device(self.device):
-            _lib.call('sad_heads_plan_create', _lib.pointer_array(arrays), self.n_heads, fi, n_feat,
-                      _lib.ctypes.byref(self._plan))
+            _lib.call('sad_heads_plan_create_dim', _lib.pointer_array(arrays), self.n_heads, fi, n_feat,
+                      feat_dim, _lib.ctypes.byref(self._plan))
         self.n_feat = n_feat
         self._ws = None
 
@@ -216,6 +278,15 @@ class Heads:
                 _lib.load().sad_heads_plan_destroy(self._plan)
         except Exception:
             pass
+
+
+def _arch(base_sd) -> str:
+    """Architecture name of a backbone state dict; unrecognised key sets are
+    treated as resnet18 so that the missing-key check names what is absent."""
+    try:
+        return arch_of_state(base_sd) if base_sd else 'resnet18'
+    except ValueError:
+        return 'resnet18'
 
 
 def _digest(tensors: List[torch.Tensor]) -> str:
@@ -258,17 +329,26 @@ class Engine:
             raise ValueError('state dict has no sub_models.<i>.* keys')
         self.indices = idx
         digests, self.backbones, feat_index = {}, [], []
+        archs = {_arch(bases[i]) for i in idx}
+        if len(archs) != 1:
+            raise ValueError(f'sub-models mix backbone architectures {sorted(archs)}')
+        self.arch = archs.pop()
         for i in idx:
-            keys = [k for k, _, kind in backbone_param_shapes()]
+            keys = [k for k, _, kind in arch_param_shapes(self.arch)]
             missing = [k for k in keys if not any(s.startswith(k + '.') for s in bases[i])]
             if missing:
                 raise KeyError(f'sub-model {i} lacks backbone tensors {missing[:3]}...')
             d = _digest([bases[i][k] for k in sorted(bases[i]) if not k.endswith('num_batches_tracked')])
             if d not in digests:
                 digests[d] = len(self.backbones)
-                self.backbones.append(Backbone(bases[i], self.device, dtype, micro_batch))
+                if self.arch == 'resnet18':  # the tuned ResNet-18 plan
+                    self.backbones.append(Backbone(bases[i], self.device, dtype, micro_batch))
+                else:
+                    self.backbones.append(ResNetBackbone(bases[i], self.arch, self.device, dtype, micro_batch))
             feat_index.append(digests[d])
-        self.heads = Heads([heads[i] for i in idx], feat_index, len(self.backbones), self.device)
+        self.num_features = arch_spec(self.arch)[2]
+        self.heads = Heads([heads[i] for i in idx], feat_index, len(self.backbones), self.device,
+                           feat_dim=self.num_features)
         self.frontend = FrontEnd(self.device, norm=norm)
         self.n_heads = len(idx)
 

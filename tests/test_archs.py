@@ -1,0 +1,42 @@
+"""Deeper timm ResNets -- host side, no GPU: the
+deterministic state dicts carry exactly timm's keys and shapes (as restated by
+the oracle), and the engine recognises the architecture from the keys."""
+import pytest
+
+from sad import weights as sw
+
+
+@pytest.mark.parametrize('name', list(sw.ARCHS))
+def test_state_dict_layout_matches_oracle(name):
+    from oracle import resnet as ores
+    ref = ores.BinaryClassifier(name).state_dict()
+    mine = {f'base.{k}': v for k, v in sw.backbone_state_dict(0, name).items()}
+    mine.update({f'head.{k}': v for k, v in sw.head_state_dict(1, sw.arch_spec(name)[2]).items()})
+    assert list(ref.keys()) == list(mine.keys())
+    for k in ref:
+        assert tuple(ref[k].shape) == tuple(mine[k].shape), k
+    assert sw.arch_of_state(sw.backbone_state_dict(0, name)) == name
+
+
+def test_resnet18_weights_unchanged_by_generalisation():
+    """resnet18's hash-seeded values depend only on its own key order."""
+    a = sw.backbone_state_dict(0)
+    b = sw.backbone_state_dict(0, 'resnet18')
+    assert all((a[k] == b[k]).all() for k in a)
+
+
+def test_unknown_arch_rejected():
+    with pytest.raises(ValueError):
+        sw.arch_spec('resnet26t')
+    bad = sw.backbone_state_dict(0)
+    bad = {k: v for k, v in bad.items() if not k.startswith('layer4.1.')}
+    with pytest.raises(ValueError):
+        sw.arch_of_state(bad)
+
+
+def test_runner_accepts_deeper_names():
+    import inference_runner as ir
+    m = ir.BinaryClassifier('resnet50', init='empty')
+    assert m.state_dict()['head.2.weight'].shape == (512, 2048)
+    with pytest.raises(ValueError):
+        ir.BinaryClassifier('vgg16', init='empty')

@@ -1,0 +1,82 @@
+"""GPU parity of the deeper timm ResNets (resnet34 BasicBlocks, resnet50
+Bottlenecks) on libsad's generic ResNet plan against the
+CPU oracle, end to end from the golden maps to the merged logits.
+
+The hash-seeded weights get BN running statistics calibrated on the test maps
+themselves (oracle in train mode, cumulative averages), so activations stay
+O(1) through 16-36 blocks.  Tolerances: fp32 mode |dlogit| <= 1e-3 (the
+north-star bar); bf16 mode pooled features relative error <= 1e-1 (reported,
+not the parity gate).  parity pinned only through the oracle (no reference
+fixture exists for these backbones)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda:0'
+
+
+def _calibrated(name, maps):
+    from oracle import frontend as ofe
+    from oracle import resnet as ores
+    from sad import weights as sw
+    sd = sw.merged_state_dict(0, 2, False, model_name=name)
+    model = ores.load_merged_state(sd, name)
+    img = ofe.resize_bilinear(maps.unsqueeze(1), (512, 512)).repeat(1, 3, 1, 1)
+    for m in model.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.reset_running_stats()
+            m.momentum = None
+    model.train()
+    with torch.no_grad():
+        model.sub_models[0].base.forward_features(img)
+        for sm in model.sub_models[1:]:
+            sm.base.load_state_dict(model.sub_models[0].base.state_dict())
+    model.eval()
+    with torch.no_grad():
+        ref = model(img)
+        feats = model.sub_models[0].base(img)
+    return model.state_dict(), ref, feats
+
+
+@pytest.fixture(scope='module')
+def maps(golden_frontend):
+    return torch.from_numpy(golden_frontend['std_map'][:3]).contiguous()
+
+
+@pytest.mark.parametrize('name', ['resnet50', 'resnet34'])
+def test_deep_resnet_vs_oracle(name, maps):
+    from sad.engine import Engine, ResNetBackbone
+    sd, ref, ref_feats = _calibrated(name, maps)
+    eng = Engine(sd, DEV, dtype='fp32', micro_batch=2)  # ragged tail: 3 = 2 + 1
+    assert eng.arch == name and len(eng.backbones) == 1 and isinstance(eng.backbones[0], ResNetBackbone)
+    _, merged = eng.forward_maps(maps.to(DEV))
+    feats = eng.backbones[0](maps.to(DEV))
+    torch.cuda.synchronize()
+    df = ((feats.cpu() - ref_feats).abs().max() / ref_feats.abs().max()).item()
+    d = (merged.cpu() - ref).abs().max().item()
+    print(f'{name} fp32: pooled rel err {df:.3e}, max|dlogit| {d:.3e}')
+    assert np.isfinite(merged.cpu().numpy()).all()
+    assert d <= 1e-3
+
+    eng16 = Engine(sd, DEV, dtype='bf16', micro_batch=3)
+    f16 = eng16.backbones[0](maps.to(DEV))
+    torch.cuda.synchronize()
+    e16 = ((f16.cpu() - ref_feats).abs().max() / ref_feats.abs().max()).item()
+    print(f'{name} bf16: pooled rel err {e16:.3e}')
+    assert e16 <= 1e-1
+
+
+def test_deep_resnet_image_entry_matches_map_entry(maps):
+    """sad_resnet_run_img on the resized image == sad_resnet_run on the map."""
+    from sad.engine import ResNetBackbone, resize
+    from sad import weights as sw
+    base = sw.backbone_state_dict(0, 'resnet50')
+    bb = ResNetBackbone(base, 'resnet50', DEV, 'fp32', micro_batch=3)
+    m = maps.to(DEV)
+    a = bb(m)
+    b = bb.forward_images(resize(m))
+    torch.cuda.synchronize()
+    err = ((a - b).abs().max() / a.abs().max()).item()
+    assert err <= 1e-5, err
