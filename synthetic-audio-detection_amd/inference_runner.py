@@ -22,8 +22,10 @@ Differences (documented in DESIGN.md):
     checkpoint missing backbone keys is an error instead of being filled from
     them;
   * extra, non-breaking flags: ``--precision {fp32,bf16}`` (default fp32 = the
-    reference's arithmetic; bf16 = throughput mode) and ``--batch-size``
-    (default 128, the reference's mini-batch at :284).
+    reference's arithmetic; bf16 = throughput mode), ``--batch-size``
+    (default 128, the reference's mini-batch at :284) and ``--model-name``
+    (default resnet18, the reference's hard-coded backbone; resnet34/50/101/152
+    run on the generic ResNet plan).
 """
 from __future__ import annotations
 
@@ -358,6 +360,8 @@ def main(argv=None):
     parser.add_argument('--precision', choices=['fp32', 'bf16'], default='fp32',
                         help='device arithmetic: fp32 (reference numerics) or bf16 (throughput)')
     parser.add_argument('--batch-size', type=int, default=128, help='windows per device launch')
+    parser.add_argument('--model-name', default='resnet18', choices=list(_weights.ARCHS),
+                        help='backbone of the merged sub-models (the reference hard-codes resnet18, :77,246)')
     args = parser.parse_args(argv)
 
     seed = 9
@@ -366,7 +370,8 @@ def main(argv=None):
     torch.manual_seed(seed)
     device = _engine._dev(args.device)
 
-    model, metadata = load_merged_model(args.merged_model, device, precision=args.precision)
+    model, metadata = load_merged_model(args.merged_model, device, backbone_name=args.model_name,
+                                        precision=args.precision)
     class_names = metadata['class_names']
     synthetic_names = class_names[:-1]
     real_name = class_names[-1]

@@ -80,3 +80,40 @@ def test_deep_resnet_image_entry_matches_map_entry(maps):
     torch.cuda.synchronize()
     err = ((a - b).abs().max() / a.abs().max()).item()
     assert err <= 1e-5, err
+
+
+def test_merger_and_runner_cli_resnet50(tmp_path, golden_frontend):
+    """model_merger.main --model-name resnet50 -> inference_runner.main
+    --model-name resnet50 on a 4-window WAV; the JSON equals summarize() of the
+    oracle's merged logits (same segments/labels, percentages within 1e-3)."""
+    import csv
+    import json
+
+    import inference_runner as ir
+    import model_merger as mm
+    from oracle import frontend as ofe
+    from sad.audio import save_pcm16
+    pcm = golden_frontend['pcm'][:4]
+    _, maps = ofe.batch_maps(pcm)
+    sd, ref, _ = _calibrated('resnet50', maps)
+    rows = []
+    for i in range(2):
+        sub = {k[len(f'sub_models.{i}.'):]: v for k, v in sd.items() if k.startswith(f'sub_models.{i}.')}
+        torch.save({'state_dict': sub}, tmp_path / f'sub{i}.pth')
+        rows.append({'model_filename': f'sub{i}.pth', 'synthetic_class': f'Syn{i}', 'real_class': 'Real'})
+    with open(tmp_path / 'm.csv', 'w', newline='') as f:
+        w = csv.DictWriter(f, fieldnames=['model_filename', 'synthetic_class', 'real_class'])
+        w.writeheader()
+        w.writerows(rows)
+    merged = str(tmp_path / 'merged.pth')
+    names = mm.main(['--submodels-folder', str(tmp_path), '--csv-file', str(tmp_path / 'm.csv'),
+                     '--model-name', 'resnet50', '--output-path', merged])
+    assert names == ['Syn0', 'Syn1', 'Real']
+    wav = str(tmp_path / 'clip.wav')
+    save_pcm16(wav, np.concatenate(list(pcm)))
+    out = str(tmp_path / 'o.json')
+    js = ir.main(['--merged-model', merged, '--audio', wav, '--output-json', out, '--model-name', 'resnet50'])
+    exp = ir.summarize(wav, list(ref), [0.0, 4.0, 8.0, 12.0], 0.5, ['Syn0', 'Syn1'], 'Real', False, 4.0)
+    assert js['segments'] == exp['segments']
+    for k, v in exp['percentages'].items():
+        assert abs(js['percentages'][k] - v) <= 1e-3, (k, js['percentages'][k], v)
