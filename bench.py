@@ -37,7 +37,9 @@ BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 # rocprof key in profiles/r01_pmc_traffic.json; 1344 TFLOP/s = the best bf16 GEMM
 # measured on this box (tools/gemm_ref.py)
 DOMINANT_VARIANT = 13
-DOMINANT_KERNEL = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1>|131072'
+DOMINANT_KERNEL = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1, false>|131072'
+# the same kernel's name in profiles taken before the epilogue-residual template flag (identical ISA)
+DOMINANT_KERNEL_OLD = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1>|131072'
 F32_PEAK_TFLOPS = 157.3
 FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats
 FE_BYTES = 256000 + 128512     # int16 PCM read + fp32 [128, 251] map written
@@ -162,7 +164,8 @@ def main():
         traffic = None
         tj = os.path.join(ROOT, 'profiles', 'r01_pmc_traffic.json')
         if os.path.exists(tj) and args.dtype == 'bf16':
-            rec = json.load(open(tj)).get(DOMINANT_KERNEL)
+            tr = json.load(open(tj))
+            rec = tr.get(DOMINANT_KERNEL) or tr.get(DOMINANT_KERNEL_OLD)
             if rec and rec.get('hbm_read_bytes') is not None:
                 traffic = rec['hbm_read_bytes'] + rec['hbm_write_bytes']
         out = {

@@ -56,7 +56,10 @@ constexpr int block_smem_bytes() {
          (block_can_pool<WC, WP, TC, TP, S, OCC>() ? 16 * TC * WC * 4 * WP : 0);
 }
 
-template <typename T, int WC, int WP, int TC, int TP, int S, int OCC>
+// RES: the epilogue adds a residual tensor (a Bottleneck's identity shortcut,
+// resnet.hip) -- its own instantiation, so the ResNet-18 kernels' register
+// allocation does not carry its loads
+template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES>
 __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_kernel(BlockConvArgs a) {
   static_assert(S == 2 || S == 3, "ring depth");
   constexpr int NW = WC * WP;
@@ -339,7 +342,29 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               v[r] = acc[i][j][r] + bb[r];
-              if (a.relu) v[r] = fmaxf(v[r], 0.f);
+              if constexpr (!RES) {
+                if (a.relu) v[r] = fmaxf(v[r], 0.f);
+              }
+            }
+            if constexpr (RES) {
+              // epilogue residual (a Bottleneck's identity shortcut): 4 channels of pixel px
+              const T* rp = (const T*)a.res + (int64_t)px * a.res_pstride + co;
+              if constexpr (sizeof(T) == 2) {
+                const uint2 q = *(const uint2*)rp;
+                v[0] += bf2f((u16)(q.x & 0xFFFF));
+                v[1] += bf2f((u16)(q.x >> 16));
+                v[2] += bf2f((u16)(q.y & 0xFFFF));
+                v[3] += bf2f((u16)(q.y >> 16));
+              } else {
+                const float4 q = *(const float4*)rp;
+                v[0] += q.x;
+                v[1] += q.y;
+                v[2] += q.z;
+                v[3] += q.w;
+              }
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (a.relu) v[r] = fmaxf(v[r], 0.f);
             }
             T* op = out + (int64_t)px * a.out_pstride + co;
             if constexpr (sizeof(T) == 2) {
@@ -363,15 +388,19 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <typename T, int WC, int WP, int TC, int TP, int S, int OCC>
+template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES_OK = false>
 static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
   constexpr int smem = block_smem_bytes<WC, WP, TC, TP, S, OCC>();
   static_assert(smem * OCC <= 160 * 1024, "LDS budget");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
+  SAD_REQUIRE(RES_OK || !a.res, "this block-conv variant has no epilogue residual (variants 13, 20, 21, 25 do)");
+  const void* kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false>;
+  if constexpr (RES_OK) {
+    if (a.res) kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true>;
+  }
+  static bool attr[2] = {false, false};
+  if (!attr[a.res != nullptr]) {
+    (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr[a.res != nullptr] = true;
   }
   constexpr int BC = 16 * TC * WC, BP = 16 * TP * WP;
   const int occupancy = OCC;
@@ -388,7 +417,15 @@ static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
   const int64_t nk = (int64_t)a.KH * a.KW * a.Cin * sizeof(T) / 128 + (a.in1 ? a.Cin1 * sizeof(T) / 128 : 0);
   SAD_REQUIRE(a.M + BP < (1ll << 31) && (tiles_p / (g / n_tc) + 1) * nk < (1ll << 31),
               "block conv: too many pixels for one launch (lower the micro-batch)");
-  hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC>), dim3((unsigned)g), dim3(64 * WC * WP), smem, s, a);
+  if constexpr (RES_OK) {
+    if (a.res) {
+      hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true>), dim3((unsigned)g), dim3(64 * WC * WP),
+                         smem, s, a);
+      SAD_CHECK_HIP(hipGetLastError());
+      return SAD_OK;
+    }
+  }
+  hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false>), dim3((unsigned)g), dim3(64 * WC * WP), smem, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }
@@ -407,7 +444,7 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
     case 10: return launch_block_t<T, 2, 2, 4, 4, 2, 2>(a, s);
     case 11: return launch_block_t<T, 1, 4, 4, 4, 3, 1>(a, s);
     case 12: return launch_block_t<T, 2, 2, 4, 4, 3, 1>(a, s);
-    case 13: return launch_block_t<T, 2, 4, 8, 4, 2, 1>(a, s);
+    case 13: return launch_block_t<T, 2, 4, 8, 4, 2, 1, true>(a, s);
     case 14: return launch_block_t<T, 2, 4, 4, 4, 2, 1>(a, s);
     case 15: return launch_block_t<T, 2, 4, 4, 4, 3, 1>(a, s);
     case 16: return launch_block_t<T, 1, 8, 4, 4, 2, 1>(a, s);
@@ -501,7 +538,7 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
     SAD_REQUIRE(halo_ok(a, dtype), "halo conv (variants 20, 21): bf16, 3x3/s1/p1, no GEMM shortcut, H, W % 16");
     return launch_halo_v(a, v, s);
   }
-  SAD_REQUIRE(!a.res, "an epilogue residual needs the halo kernel (variant 20)");
+  SAD_REQUIRE(!a.res || a.res_pstride % 4 == 0, "residual pixel stride must keep 4-channel alignment");
   return dtype == SAD_BF16 ? launch_block_v<u16>(a, v, s) : launch_block_v<float>(a, v, s);
 }
 

@@ -12,13 +12,14 @@
 //   Bottleneck:  T1 = relu(conv1x1(X));  T2 = relu(conv3x3/s(T1))
 //                downsample block: Y = relu(conv1x1(T2) + ds(X)) as one GEMM
 //                (K = width + cin, shortcut pixels (oy*s, ox*s) of X)
-//                identity block:   Y = relu(conv1x1(T2) + X) on the implicit
-//                     GEMM with its epilogue residual (identity columns would
-//                     add 4*width K per pixel: +94 % of the block's FLOPs)
+//                identity block:   Y = relu(conv1x1(T2) + X), X added in the
+//                     block-conv epilogue (block_conv_kernel<..., RES = true>;
+//                     identity columns would add 4*width K per pixel: +94 % of
+//                     the block's FLOPs)
 //   global average pool -> feats [B, num_features] fp32
 // Every conv is one launch of launch_block_conv (tile variant picked by
 // default_block_variant: the resident-weight / halo kernels for the 3x3/s1
-// convs that qualify) or launch_conv; BN is folded into weights and bias.
+// convs that qualify); BN is folded into weights and bias.
 #include <math.h>
 
 #include <algorithm>
@@ -202,7 +203,8 @@ extern "C" int sad_resnet_workspace_size(const sad_resnet_plan* p, int64_t mb, s
 
 // one conv (+ optional GEMM shortcut of `sc`) on the block-conv kernels
 static int rn_block_conv(const sad_resnet_plan* p, const ConvW& c, const void* x, int64_t n, int H, int stride,
-                         const void* sc, int Hs, int sc_cin, int sc_stride, void* y, hipStream_t s) {
+                         const void* sc, int Hs, int sc_cin, int sc_stride, void* y, hipStream_t s,
+                         const void* res = nullptr) {
   const int pad = c.k / 2;
   const int Ho = (H + 2 * pad - c.k) / stride + 1;
   BlockConvArgs a{};
@@ -224,6 +226,8 @@ static int rn_block_conv(const sad_resnet_plan* p, const ConvW& c, const void* x
   a.wt = c.w;
   a.wt_ld = c.ld;
   a.bias = c.b;
+  a.res = res;  // epilogue residual (NHWC, c.cout channels)
+  a.res_pstride = c.cout;
   a.out = y;
   a.out_pstride = c.cout;
   a.Ho = a.Wo = Ho;
@@ -255,26 +259,7 @@ static int rn_chunk(const sad_resnet_plan* p, const float* map, const float* img
       if (b.has_ds) {
         if ((rc = rn_block_conv(p, b.c3, T2, n, Ho, 1, X, H, C, b.stride, Y, s))) return rc;
       } else {
-        ConvArgs a{};
-        a.in = T2;
-        a.in_pstride = b.width;
-        a.N = (int)n;
-        a.H = a.W = Ho;
-        a.Cin = b.width;
-        a.wt = b.c3.w;
-        a.bias = b.c3.b;
-        a.res = X;
-        a.res_pstride = C;
-        a.out = Y;
-        a.out_pstride = b.cout;
-        a.Ho = a.Wo = Ho;
-        a.Cout = b.cout;
-        a.KH = a.KW = 1;
-        a.stride = 1;
-        a.pad = 0;
-        a.relu = 1;
-        a.M = n * Ho * Ho;
-        if ((rc = launch_conv(a, p->dtype, s))) return rc;
+        if ((rc = rn_block_conv(p, b.c3, T2, n, Ho, 1, nullptr, 0, 0, 1, Y, s, X))) return rc;
       }
     }
     std::swap(X, Y);

@@ -93,3 +93,36 @@ def test_block_conv_variants(name, N, H, Cin, Cout, stride, sc, variants):
             first = out
         else:
             assert torch.equal(out, first), f'variant {v} differs bitwise from variant {variants[0]}'
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_bottleneck_1x1_epilogue_residual(dtype):
+    """Variant 13 with RES: a Bottleneck's conv3 (1x1) + identity shortcut added
+    in the epilogue (resnet.hip), ragged pixel tail (M = 588), and the same
+    conv with the downsample as GEMM columns (K = width + cin)."""
+    from sad.engine import block_conv
+    g = torch.Generator().manual_seed(55)
+    N, H, width, cout = 3, 14, 128, 512
+    x = torch.randn(N, H, H, width, generator=g).to(torch.bfloat16)
+    res = torch.randn(N, H, H, cout, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, width, generator=g) * (2.0 / width) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(cout, generator=g) * 0.1
+    ref = _ref(x, w, bias, 1, None, 1, res, True, k=1)
+    out = block_conv(x.to(DEV, dtype), w.to(DEV, dtype), bias.to(DEV), 1, 0, relu=True, variant=13,
+                     res=res.to(DEV, dtype), k=1)
+    torch.cuda.synchronize()
+    if dtype == torch.float32:
+        assert (out.cpu() - ref).abs().max().item() <= 1e-4
+    else:
+        _check(out.cpu(), ref)
+    # downsample folded as shortcut columns over a 2x larger source (stride 2)
+    sc = torch.randn(N, 2 * H, 2 * H, 256, generator=g).to(torch.bfloat16)
+    w2 = (torch.randn(cout, width + 256, generator=g) * (2.0 / (width + 256)) ** 0.5).to(torch.bfloat16)
+    ref2 = _ref(x, w2, bias, 1, sc, 2, None, True, k=1)
+    out2 = block_conv(x.to(DEV, dtype), w2.to(DEV, dtype), bias.to(DEV), 1, 0, sc=sc.to(DEV, dtype), sc_stride=2,
+                      relu=True, k=1)
+    torch.cuda.synchronize()
+    if dtype == torch.float32:
+        assert (out2.cpu() - ref2).abs().max().item() <= 1e-4
+    else:
+        _check(out2.cpu(), ref2)
