@@ -281,6 +281,7 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
   return s;
 }
 
+constexpr int kNormRegs = 32;  // values per thread held in registers (1024 threads: maps up to 32768)
 __global__ __launch_bounds__(1024) void fe_normalize_kernel(float* db_io, int count,
                                                              float top_db, float* map_out) {
   __shared__ double red[16];
@@ -289,6 +290,54 @@ __global__ __launch_bounds__(1024) void fe_normalize_kernel(float* db_io, int co
   float* x = db_io + seg * count;
   float* y = map_out + seg * count;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (count <= kNormRegs * (int)blockDim.x) {
+    // one HBM read: the segment's values stay in registers (32 per thread for
+    // the 128 x 251 map); every reduction visits them in the same per-thread
+    // order as the multi-pass loop below, so the results are identical
+    float v[kNormRegs];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < kNormRegs; ++k) {
+      const int i = tid + k * (int)blockDim.x;
+      v[k] = i < count ? x[i] : -INFINITY;
+      mx = fmaxf(mx, v[k]);
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0) redf[wave] = mx;
+    __syncthreads();
+    mx = redf[0];
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) mx = fmaxf(mx, redf[i]);
+    const float floor_db = top_db >= 0.f ? mx - top_db : -INFINITY;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kNormRegs; ++k) {
+      const int i = tid + k * (int)blockDim.x;
+      if (i < count) {
+        v[k] = fmaxf(v[k], floor_db);
+        if (x != y) x[i] = v[k];  // caller asked for the clamped dB map
+        s += (double)v[k];
+      }
+    }
+    const double mean = block_sum_d(s, red) / count;
+    const float mean_f = (float)mean;
+    double ss = 0.0;
+#pragma unroll
+    for (int k = 0; k < kNormRegs; ++k) {
+      const int i = tid + k * (int)blockDim.x;
+      if (i < count) {
+        const double d = (double)v[k] - mean;
+        ss += d * d;
+      }
+    }
+    const double var = block_sum_d(ss, red) / (count - 1);
+    const float denom = (float)sqrt(var) + 1e-6f;
+#pragma unroll
+    for (int k = 0; k < kNormRegs; ++k) {
+      const int i = tid + k * (int)blockDim.x;
+      if (i < count) y[i] = (v[k] - mean_f) / denom;
+    }
+    return;
+  }
   float mx = -INFINITY;
   for (int i = tid; i < count; i += blockDim.x) mx = fmaxf(mx, x[i]);
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
