@@ -513,17 +513,38 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
     src_row(iy_hi, t1, yhi, tl);
     const int nh = yhi - ylo + 1;
     if (nh <= STEM_HROWS) {
-      // x-lerp of map rows ylo..yhi for every image column
-      for (int i = tid; i < nh * 512; i += 256) {
-        const int r = i >> 9, ix = i & 511;
+      // x-lerp of map rows ylo..yhi for every image column: a thread owns
+      // columns tid and tid + 256 and issues all its rows' gathers before the
+      // first use (one memory latency per workgroup instead of one per row)
+      int x0[2], x1[2];
+      float lx[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int ix = tid + 256 * c;
         float fx = sw * (ix + 0.5f) - 0.5f;
         fx = fx < 0.f ? 0.f : fx;
-        const int x0 = min((int)floorf(fx), a.mw - 1), x1 = min(x0 + 1, a.mw - 1);
-        const float lx = fminf(fmaxf(fx - x0, 0.f), 1.f);
-        const float* mr = map + (ylo + r) * a.mw;
-        s_u[i] = (1.f - lx) * mr[x0] + lx * mr[x1];
+        x0[c] = min((int)floorf(fx), a.mw - 1);
+        x1[c] = min(x0[c] + 1, a.mw - 1);
+        lx[c] = fminf(fmaxf(fx - x0[c], 0.f), 1.f);
       }
+      float g0[STEM_HROWS][2], g1[STEM_HROWS][2];
+#pragma unroll
+      for (int r = 0; r < STEM_HROWS; ++r) {
+        const float* mr = map + (ylo + min(r, nh - 1)) * a.mw;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          g0[r][c] = mr[x0[c]];
+          g1[r][c] = mr[x1[c]];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < STEM_HROWS; ++r)
+        if (r < nh) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c) s_u[r * 512 + tid + 256 * c] = (1.f - lx[c]) * g0[r][c] + lx[c] * g1[r][c];
+        }
       __syncthreads();
+#pragma unroll 4
       for (int i = tid; i < NBR * STEM_BPITCH; i += 256) {
         const int tr = i / STEM_BPITCH, tc = i - tr * STEM_BPITCH;
         const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
