@@ -51,20 +51,20 @@ def segment_image(wave: torch.Tensor, mask=None, box=None) -> torch.Tensor:
 
 
 class TrainModel(nn.Module):
-    """timm resnet18(num_classes=0) + the trainer's (unused) head."""
+    """timm resnet18 / resnet34 (num_classes=0) + the trainer's (unused) head."""
 
-    def __init__(self):
+    def __init__(self, model_name: str = 'resnet18'):
         super().__init__()
-        self.base = ores.create_model('resnet18', num_classes=0)
+        self.base = ores.create_model(model_name, num_classes=0)
         self.head = ores.make_head(512)
 
     def forward(self, x):
         return self.base(x)  # timm forward: pooled features (head unused, quirk C1)
 
 
-def build(base_sd: dict, head_sd: dict, lr: float = 1e-3):
+def build(base_sd: dict, head_sd: dict, lr: float = 1e-3, model_name: str = 'resnet18'):
     """(model, optimizer) as at submodel_trainer.py:606-660."""
-    m = TrainModel()
+    m = TrainModel(model_name)
     m.base.load_state_dict({k: v for k, v in base_sd.items()}, strict=True)
     m.head.load_state_dict({k: v for k, v in head_sd.items()}, strict=True)
     for p in m.parameters():

@@ -38,8 +38,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from .engine import MAP_H, MAP_W, Backbone, FrontEnd, _dev
-from .weights import HEAD_LAYOUT, backbone_param_shapes
+from .engine import MAP_H, MAP_W, Backbone, FrontEnd, ResNetBackbone, _dev
+from .weights import HEAD_LAYOUT, arch_param_shapes, arch_spec, backbone_param_shapes
 
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
@@ -51,11 +51,12 @@ WEIGHT_DECAY = 0.01
 MAX_GRAD_NORM = 0.5
 
 
-def block_table():
-    """[(prefix, cin, cout, stride, has_downsample)] of timm resnet18."""
+def block_table(layers=(2, 2, 2, 2)):
+    """[(prefix, cin, cout, stride, has_downsample)] of a timm BasicBlock ResNet
+    (resnet18 by default; resnet34 = (3, 4, 6, 3))."""
     out, inp = [], 64
     for li, planes in enumerate((64, 128, 256, 512)):
-        for b in range(2):
+        for b in range(layers[li]):
             s = 2 if (b == 0 and li > 0) else 1
             out.append((f'layer{li + 1}.{b}', inp, planes, s, b == 0 and li > 0))
             inp = planes
@@ -65,10 +66,17 @@ def block_table():
 BLOCKS = block_table()
 
 
-def param_layout():
+def _basic_layers(model_name: str):
+    block, layers, _ = arch_spec(model_name)
+    if block != 'basic':
+        raise ValueError(f'the device trainer runs BasicBlock ResNets (resnet18/34), not {model_name!r}')
+    return layers
+
+
+def param_layout(model_name: str = 'resnet18'):
     """[(name, shape)] of the backbone's parameters in timm ``parameters()`` order."""
     out = []
-    for key, shape, kind in backbone_param_shapes():
+    for key, shape, kind in arch_param_shapes(model_name):
         if kind == 'conv':
             out.append((f'{key}.weight', shape))
         else:
@@ -88,7 +96,7 @@ def head_keys():
 
 
 # --------------------------------------------------------------- initialisation
-def init_state_dict(seed: int = 42):
+def init_state_dict(seed: int = 42, model_name: str = 'resnet18'):
     """Initial trainer model, ``torch.manual_seed(seed)`` then
     ``timm.create_model('resnet18', pretrained=False, num_classes=0)`` and the
     MLP head (``submodel_trainer.py:599-625``), reproduced by making the same CPU
@@ -99,11 +107,11 @@ def init_state_dict(seed: int = 42):
     timm is not installed here, so bit-identity with it is unpinned.
     Returns (backbone_sd, head_sd) with timm / nn.Sequential keys."""
     g = torch.Generator().manual_seed(seed)
-    layout = backbone_param_shapes()
+    layout = arch_param_shapes(model_name)
     convs = {k: torch.empty(s) for k, s, kind in layout if kind == 'conv'}
     # construction order: conv1, then per stage: downsample.0, block convs
     order = ['conv1']
-    for prefix, _, _, _, has_ds in BLOCKS:
+    for prefix, _, _, _, has_ds in block_table(_basic_layers(model_name)):
         if has_ds:
             order.append(f'{prefix}.downsample.0')
         order += [f'{prefix}.conv1', f'{prefix}.conv2']
@@ -178,16 +186,18 @@ class TrainFrontEnd:
 
 # ------------------------------------------------------------------- network
 class TrainNet:
-    """timm resnet18 (+ the unused MLP head) in train mode on one device."""
+    """timm resnet18 / resnet34 (+ the unused MLP head) in train mode on one device."""
 
     def __init__(self, base_sd: Dict[str, torch.Tensor], head_sd: Dict[str, torch.Tensor], device='cuda',
-                 dtype: str = 'bf16'):
+                 dtype: str = 'bf16', model_name: str = 'resnet18'):
         self.device = _dev(device)
+        self.model_name = model_name
+        self.blocks = block_table(_basic_layers(model_name))
         self.dtype = dtype
         self._dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
         self.tdtype = torch.bfloat16 if dtype == 'bf16' else torch.float32
         self.es = 2 if dtype == 'bf16' else 4
-        layout = param_layout()
+        layout = param_layout(model_name)
         self.names = [n for n, _ in layout]
         sizes = [int(np.prod(s)) for _, s in layout]
         offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
@@ -200,7 +210,7 @@ class TrainNet:
             self.params[n] = self.pflat[a:b].view(s)
             self.grads[n] = self.gflat[a:b].view(s)
             self.params[n].copy_(torch.as_tensor(base_sd[n], dtype=torch.float32))
-        self.bn_keys = [k for k, _, kind in backbone_param_shapes() if kind == 'bn']
+        self.bn_keys = [k for k, _, kind in arch_param_shapes(model_name) if kind == 'bn']
         self.running = {}
         self.nbt = {}
         for k in self.bn_keys:
@@ -344,7 +354,7 @@ class TrainNet:
             _lib.call('sad_bn_relu_maxpool_run', _lib.ptr(raw), B, 256, 256, 64, self._dt, _lib.ptr(st), _lib.ptr(a), s)
         del raw
         saved = {}
-        for prefix, cin, cout, stride, has_ds in BLOCKS:
+        for prefix, cin, cout, stride, has_ds in self.blocks:
             c1 = self._conv(a, self.packed(f'{prefix}.conv1', 0), cout, 3, stride, 1)
             st1 = self._bn_stats(c1, f'{prefix}.bn1')
             a1 = self._bn_apply(c1, st1, relu=True)
@@ -372,7 +382,7 @@ class TrainNet:
         layer4 into ``self.grads`` (overwritten, as after zero_grad), layer3 (if
         3 in layers) into ``grads3`` (overwritten; the caller folds them into the
         accumulating .grad, quirk C4)."""
-        order = [b for b in reversed(BLOCKS) if int(b[0][5]) in layers]
+        order = [b for b in reversed(self.blocks) if int(b[0][5]) in layers]
         dy, dpool = None, dfeat
         for bi, (prefix, cin, cout, stride, has_ds) in enumerate(order):
             sv = saved[prefix]
@@ -412,7 +422,7 @@ class TrainNet:
     def base_state_dict(self) -> "OrderedDict[str, torch.Tensor]":
         """timm-keyed backbone state dict (CPU), parameters + BN buffers."""
         sd = OrderedDict()
-        for key, shape, kind in backbone_param_shapes():
+        for key, shape, kind in arch_param_shapes(self.model_name):
             if kind == 'conv':
                 sd[f'{key}.weight'] = self.params[f'{key}.weight'].detach().cpu().clone()
             else:
@@ -432,10 +442,12 @@ class TrainNet:
             sd[f'head.{k}'] = v.clone()
         return sd
 
-    def eval_backbone(self, micro_batch: int = 64) -> Backbone:
+    def eval_backbone(self, micro_batch: int = 64):
         """``model.eval()`` forward: the inference plan (BN folded with the
         current running statistics)."""
-        return Backbone(self.base_state_dict(), self.device, self.dtype, micro_batch)
+        if self.model_name == 'resnet18':
+            return Backbone(self.base_state_dict(), self.device, self.dtype, micro_batch)
+        return ResNetBackbone(self.base_state_dict(), self.model_name, self.device, self.dtype, micro_batch)
 
 
 def ce_loss(feats: torch.Tensor, targets: torch.Tensor, scale: float = 0.0, want_grad: bool = False,
@@ -460,8 +472,8 @@ class Trainer:
     accumulator, with an optional process group (DDP over RCCL)."""
 
     def __init__(self, base_sd, head_sd, device='cuda', dtype: str = 'bf16', lr: float = 1e-3, group=None,
-                 world: int = 1):
-        self.net = TrainNet(base_sd, head_sd, device, dtype)
+                 world: int = 1, model_name: str = 'resnet18'):
+        self.net = TrainNet(base_sd, head_sd, device, dtype, model_name)
         self.device = self.net.device
         self.group, self.world = group, world
         a4, b4 = self.net.range4

@@ -30,8 +30,8 @@ Differences (documented in DESIGN.md / INTEGRATION.md):
   * ``--num_gpus > 1`` = one process per GPU (torchrun) over RCCL instead of
     DataParallel threads: each rank loads ``--batch-size`` files per step;
     per-replica BN statistics as in DP; gradients all-reduced.
-  * no CPU fallback; ``--model-name`` must be resnet18 (the device kernels
-    implement timm's BasicBlock resnet18, the only backbone inference uses).
+  * no CPU fallback; ``--model-name`` must be a BasicBlock ResNet (resnet18,
+    resnet34): the device backward kernels implement timm's BasicBlock.
   * extra flags: ``--precision {bf16,fp32}`` (default bf16 = throughput mode),
     ``--max-steps`` (stop an epoch early; benchmarking).
   * TensorBoard is optional (not installed here): scalars are logged instead.
@@ -61,7 +61,7 @@ warnings.filterwarnings("ignore")
 
 SEGMENT_LENGTH = 4 * 32000
 # timm.list_models('resnet*') is unavailable offline: the choices the reference's
-# CLI accepts for --model-name (timm 0.9 names); only resnet18 runs on the device.
+# CLI accepts for --model-name (timm 0.9 names); resnet18 / resnet34 run on the device.
 RESNET_MODELS = ['resnet10t', 'resnet14t', 'resnet18', 'resnet18d', 'resnet26', 'resnet26d', 'resnet26t',
                  'resnet32ts', 'resnet33ts', 'resnet34', 'resnet34d', 'resnet50', 'resnet50_gn', 'resnet50d',
                  'resnet50t', 'resnet51q', 'resnet61q', 'resnet101', 'resnet101d', 'resnet152', 'resnet152d',
@@ -451,8 +451,9 @@ def main(argv=None):
         logging.error(f"Requested number of GPUs ({args.num_gpus}) is greater than available GPUs "
                       f"({torch.cuda.device_count()})")
         sys.exit(1)
-    if args.model_name != 'resnet18':
-        raise NotImplementedError(f'--model-name {args.model_name}: the MI355X kernels implement resnet18 only')
+    if args.model_name not in ('resnet18', 'resnet34'):
+        raise NotImplementedError(f'--model-name {args.model_name}: the MI355X trainer kernels implement the '
+                                  'BasicBlock ResNets (resnet18, resnet34)')
     if not torch.cuda.is_available():
         raise RuntimeError('submodel_trainer runs on MI355X GPUs only (no CPU path)')
     torch.cuda.set_device(local)
@@ -471,8 +472,9 @@ def main(argv=None):
 
     from sad import train as st
     logging.info("Creating model with RANDOM weights...")
-    base_sd, head_sd = st.init_state_dict(args.seed)
-    trainer = st.Trainer(base_sd, head_sd, device, args.precision, lr=args.lr, group=group, world=world)
+    base_sd, head_sd = st.init_state_dict(args.seed, args.model_name)
+    trainer = st.Trainer(base_sd, head_sd, device, args.precision, lr=args.lr, group=group, world=world,
+                         model_name=args.model_name)
     frontend = st.TrainFrontEnd(device, args.precision)
     model = DeviceModel(trainer, frontend, rank, world, group)
 

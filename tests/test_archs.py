@@ -40,3 +40,15 @@ def test_runner_accepts_deeper_names():
     assert m.state_dict()['head.2.weight'].shape == (512, 2048)
     with pytest.raises(ValueError):
         ir.BinaryClassifier('vgg16', init='empty')
+
+
+def test_trainer_tables_resnet34():
+    from sad import train as st
+    blocks = st.block_table(sw.ARCHS['resnet34'][1])
+    assert [b[0] for b in blocks][:4] == ['layer1.0', 'layer1.1', 'layer1.2', 'layer2.0']
+    assert sum(b[4] for b in blocks) == 3 and len(blocks) == 16
+    base, head = st.init_state_dict(42, 'resnet34')
+    assert list(base) == list(sw.backbone_state_dict(0, 'resnet34'))
+    assert all((base[f'{b[0]}.bn2.weight'] == 0).all() for b in blocks)  # timm zero_init_last
+    with pytest.raises(ValueError):
+        st.init_state_dict(42, 'resnet50')

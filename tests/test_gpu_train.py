@@ -106,7 +106,7 @@ def test_train_forward_fp32(model_sd):
         assert int(sd[f'{k}.num_batches_tracked']) == int(bn.num_batches_tracked)
 
 
-def _run_steps(model_sd, dtype, n_steps, unfreeze_at=None, lr=1e-3, sync=True):
+def _run_steps(model_sd, dtype, n_steps, unfreeze_at=None, lr=1e-3, sync=True, model_name='resnet18'):
     """n_steps of the device trainer and the oracle on the same batch.  With
     ``sync`` the oracle's layer4 weights are reset to the device's before every
     step after the first, so each step's gradients are compared from identical
@@ -120,8 +120,8 @@ def _run_steps(model_sd, dtype, n_steps, unfreeze_at=None, lr=1e-3, sync=True):
     fe = TrainFrontEnd(DEV, dtype)
     img = fe(w.to(DEV))
     targets = torch.tensor([0, 1, 1, 0])
-    tr = Trainer(base, head, DEV, dtype, lr=lr)
-    m, opt = otr.build(base, head, lr=lr)
+    tr = Trainer(base, head, DEV, dtype, lr=lr, model_name=model_name)
+    m, opt = otr.build(base, head, lr=lr, model_name=model_name)
     x_ref = _oracle_inputs(img)
     out = []
     for step in range(n_steps):
@@ -242,3 +242,20 @@ def test_train_ddp_matches_single_process_math(model_sd):
     torch.nn.CrossEntropyLoss()(outs, targets).backward()
     gr = torch.cat([p.grad.flatten() for n, p in m.base.named_parameters() if n.startswith('layer4.')])
     assert _rel(g_sum.cpu(), gr) <= 5e-3
+
+
+def test_train_step_resnet34_fp32():
+    """--model-name resnet34 (BasicBlock, layers 3-4-6-3) on the same trainer
+    kernels: one step's loss, clip norm and layer4 gradients vs autograd."""
+    from sad import train as st
+    from sad import weights as sw
+    sd = (sw.backbone_state_dict(7, 'resnet34'), st.init_state_dict(42)[1])
+    tr, m, out = _run_steps(sd, 'fp32', 1, model_name='resnet34')
+    o = out[0]
+    print(f"resnet34 loss {o['loss']:.6f} vs {o['rloss']:.6f}; norm {o['norm'][0]:.6f} vs {o['rnorm']:.6f}")
+    assert abs(o['loss'] - o['rloss']) <= 1e-4 * abs(o['rloss'])
+    assert abs(o['norm'][0].item() - o['rnorm']) <= 1e-3 * o['rnorm']
+    assert set(o['rg']) == {n for n in o['g'] if n.startswith('layer4.')}
+    for name, gr in o['rg'].items():
+        assert _rel(o['g'][name], gr) <= 5e-3, name
+    assert len([b for b in tr.net.blocks if b[0].startswith('layer3.')]) == 6
