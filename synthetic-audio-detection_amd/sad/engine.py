@@ -190,7 +190,7 @@ class ResNetBackbone:
         self._dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
         # the widest activation (layer1 of a Bottleneck net: 128x128x256) must
         # stay under the kernels' 2 GiB buffer-addressing range
-        self.micro_batch = max(1, min(micro_batch, 64))
+        self.micro_batch = max(1, min(micro_batch, 128 if dtype == 'bf16' else 64))
         arrays = []
         for key, _shape, kind in arch_param_shapes(model_name):
             if kind == 'conv':
