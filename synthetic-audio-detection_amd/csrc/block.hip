@@ -26,6 +26,8 @@
 //  * one K-step = one filter tap (or shortcut chunk) x 128 B of channels
 //    (64 bf16 / 32 f32), 8 x 16-B chunks per pixel row, XOR-swizzled through
 //    the DMA source address (LDS-DMA writes lane-linearly).
+#include <type_traits>
+
 #include "common.hpp"
 #include "igemm.hpp"
 #include "kernels.hpp"
@@ -334,6 +336,17 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
       for (int j = 0; j < TP; ++j) {
         const int px = ctile * BP + wp * 16 * TP + j * 16 + fr;
         if (out != nullptr && px < M) {
+          // epilogue residual (a Bottleneck's identity shortcut): the pixel's TC
+          // 4-channel groups are loaded together, before any of its stores (the
+          // compiler cannot move a load above a store that may alias it, so
+          // interleaved loads would each wait for the stores before them)
+          using RV = typename std::conditional<sizeof(T) == 2, uint2, float4>::type;
+          RV rres[RES ? TC : 1];
+          if constexpr (RES) {
+            const T* rp = (const T*)a.res + (int64_t)px * a.res_pstride + c0 + wc * 16 * TC + fg * 4;
+#pragma unroll
+            for (int i = 0; i < TC; ++i) rres[i] = *(const RV*)(rp + i * 16);
+          }
 #pragma unroll
           for (int i = 0; i < TC; ++i) {
             const int co = c0 + wc * 16 * TC + i * 16 + fg * 4;
@@ -347,16 +360,14 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
               }
             }
             if constexpr (RES) {
-              // epilogue residual (a Bottleneck's identity shortcut): 4 channels of pixel px
-              const T* rp = (const T*)a.res + (int64_t)px * a.res_pstride + co;
               if constexpr (sizeof(T) == 2) {
-                const uint2 q = *(const uint2*)rp;
+                const uint2 q = rres[i];
                 v[0] += bf2f((u16)(q.x & 0xFFFF));
                 v[1] += bf2f((u16)(q.x >> 16));
                 v[2] += bf2f((u16)(q.y & 0xFFFF));
                 v[3] += bf2f((u16)(q.y >> 16));
               } else {
-                const float4 q = *(const float4*)rp;
+                const float4 q = rres[i];
                 v[0] += q.x;
                 v[1] += q.y;
                 v[2] += q.z;
