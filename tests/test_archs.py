@@ -52,3 +52,14 @@ def test_trainer_tables_resnet34():
     assert all((base[f'{b[0]}.bn2.weight'] == 0).all() for b in blocks)  # timm zero_init_last
     with pytest.raises(ValueError):
         st.init_state_dict(42, 'resnet50')
+
+
+def test_bench_arch_flop_counts():
+    """tools/bench_arch.py's algorithmic FLOPs: resnet18 = SURVEY 8(d)'s 18.95
+    GFLOP per 512x512 segment; resnet50 = timm's 4.11 GMAC at 224^2 x (512/224)^2."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tools'))
+    from bench_arch import backbone_flop
+    assert abs(backbone_flop('resnet18') / 1e9 - 18.95) < 0.01
+    assert abs(backbone_flop('resnet50') / 2e9 / (512 / 224) ** 2 - 4.09) < 0.05
