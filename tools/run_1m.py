@@ -34,7 +34,9 @@ import torch.distributed as dist  # noqa: E402
 SEG = 128000
 
 
-def main():
+def main(argv=None, return_logits: bool = False):
+    """Runs the shard; with ``return_logits`` (in-process callers, e.g. the GPU
+    test) returns (the JSON record, gathered merged logits on the CPU) on rank 0."""
     ap = argparse.ArgumentParser()
     ap.add_argument('--total', type=int, default=1_000_000)
     ap.add_argument('--chunk', type=int, default=4096, help='segments per device batch')
@@ -42,7 +44,7 @@ def main():
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--micro-batch', type=int, default=512)
     ap.add_argument('--host-fed', action='store_true', help='PCM from pinned host memory (H2D inside the timing)')
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -131,9 +133,10 @@ def main():
         t = torch.tensor([inf_s, t_loop, t_gather], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         inf_s, t_loop, t_gather = t.tolist()
+    rec = None
     if rank == 0:
         finite = bool(torch.isfinite(allz).all().item())
-        print(json.dumps({
+        rec = {
             'metric': '4s@32kHz segments/sec end-to-end (mel+ResNet+ensemble), 1M-segment shard (configs[3])'
                       + (', host-fed (pinned H2D, PCIe-inclusive wall clock)' if args.host_fed else ''),
             'value': round(args.total / (inf_s + t_gather), 1), 'unit': 'segments/s', 'n_gpus': world,
@@ -141,9 +144,13 @@ def main():
             'inference_s_max_rank': round(inf_s, 3), 'allgather_s': round(t_gather, 4),
             'synthesis_s_rank0_excluded': round(gen_s, 3), 'wall_loop_s_max_rank': round(t_loop, 3),
             'gathered_rows': int(allz.shape[0]), 'all_finite': finite,
-            'logits_checksum': round(float(allz.double().sum().item()), 3)}), flush=True)
+            'logits_checksum': round(float(allz.double().sum().item()), 3)}
+        print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if return_logits:
+        return rec, allz.cpu()
+    return rec
 
 
 if __name__ == '__main__':
