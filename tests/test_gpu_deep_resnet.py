@@ -117,3 +117,65 @@ def test_merger_and_runner_cli_resnet50(tmp_path, golden_frontend):
     assert js['segments'] == exp['segments']
     for k, v in exp['percentages'].items():
         assert abs(js['percentages'][k] - v) <= 1e-3, (k, js['percentages'][k], v)
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def _emulated_bf16_features(model, img):
+    """The bf16 plan's arithmetic on the CPU: BN folded into each conv in
+    float64, weights rounded once to bf16, activations rounded to bf16 after
+    every conv (+ shortcut) + ReLU, fp32 accumulation; the stem sums the 3
+    identical input channels (resnet.hip / api.hip fold_stem)."""
+    import torch.nn.functional as F
+
+    def fold(conv, bn):
+        s = bn.weight.double() / torch.sqrt(bn.running_var.double() + 1e-5)
+        w = _bf((conv.weight.double() * s.view(-1, 1, 1, 1)).float())
+        b = (bn.bias.double() - bn.running_mean.double() * s).float()
+        return w, b
+
+    base = model.base
+    w, b = fold(base.conv1, base.bn1)
+    x = F.conv2d(_bf(img[:, :1]), w.sum(1, keepdim=True), b, stride=2, padding=3)
+    x = _bf(F.max_pool2d(F.relu(x), 3, 2, 1))
+    for li in range(1, 5):
+        for blk in getattr(base, f'layer{li}'):
+            w1, b1 = fold(blk.conv1, blk.bn1)
+            w2, b2 = fold(blk.conv2, blk.bn2)
+            w3, b3 = fold(blk.conv3, blk.bn3)
+            t = _bf(F.relu(F.conv2d(x, w1, b1)))
+            t = _bf(F.relu(F.conv2d(t, w2, b2, stride=blk.conv2.stride, padding=1)))
+            y = F.conv2d(t, w3, b3)
+            if blk.downsample is not None:
+                wd, bd = fold(blk.downsample[0], blk.downsample[1])
+                y = y + F.conv2d(x, wd, bd, stride=blk.downsample[0].stride)
+            else:
+                y = y + x
+            x = _bf(F.relu(y))
+    return x.mean(dim=(2, 3))
+
+
+def test_resnet50_bf16_vs_emulated_oracle(maps):
+    """bf16 mode against the same arithmetic emulated on the CPU.  Measured:
+    the emulation itself sits 6.9e-2 (relative, pooled features) from the fp32
+    oracle and the GPU 8.0e-2 from the emulation -- bf16 rounding flips from a
+    different fp32 summation order grow through the 16 Bottlenecks as much as
+    the bf16 rounding itself, so the bar is "same order as the inherent bf16
+    noise" (a wrong weight layout or tap order gives O(1) errors)."""
+    from oracle import frontend as ofe
+    from sad.engine import Engine
+    sd, _, ref_fp32 = _calibrated('resnet50', maps)
+    from oracle import resnet as ores
+    model = ores.load_merged_state(sd, 'resnet50')
+    img = ofe.resize_bilinear(maps.unsqueeze(1), (512, 512)).repeat(1, 3, 1, 1)
+    with torch.no_grad():
+        emu = _emulated_bf16_features(model.sub_models[0], img)
+    eng = Engine(sd, DEV, dtype='bf16', micro_batch=3)
+    f16 = eng.backbones[0](maps.to(DEV))
+    torch.cuda.synchronize()
+    e_emu = ((f16.cpu() - emu).abs().max() / emu.abs().max()).item()
+    e_emu_fp32 = ((emu - ref_fp32).abs().max() / ref_fp32.abs().max()).item()
+    print(f'resnet50 bf16 vs emulated {e_emu:.3e}; emulated vs fp32 oracle {e_emu_fp32:.3e}')
+    assert e_emu <= max(2.5 * e_emu_fp32, 2e-2)
