@@ -181,7 +181,7 @@ def main():
                        'micro_batch': args.micro_batch, 'parallelism': f'dp{world}'},
             'roofline': {'bound': 'mfma',
                          'kernel': 'sad::block_conv_kernel 256x256 tile (variant 13): the layer3 + layer4 convs, '
-                                   '8 launches per micro-batch, 33% of the step',
+                                   '8 launches per micro-batch, about 35% of the step',
                          'achieved': round(k_tf, 1), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(k_tf / peak, 4),
                          'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, '
                                                              'profiles/r01_pmc_traffic.json)',
