@@ -33,7 +33,7 @@ SEG = 128000
 BACKBONE_FLOP = 18.13e9        # ResNet-18 @512^2 with conv1's 3 identical channels folded (reference: 18.95e9)
 REF_BACKBONE_FLOP = 18.95e9
 BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
-# The dominant kernel (33% of the step, profiles/r01_bench_kernels_44k.md) and its
+# The dominant kernel (36% of the step, profiles/r01_bench_kernels_final.md) and its
 # rocprof key in profiles/r01_pmc_traffic.json; 1344 TFLOP/s = the best bf16 GEMM
 # measured on this box (tools/gemm_ref.py)
 DOMINANT_VARIANT = 13
