@@ -4,9 +4,9 @@ CPU oracle, end to end from the golden maps to the merged logits.
 
 The hash-seeded weights get BN running statistics calibrated on the test maps
 themselves (oracle in train mode, cumulative averages), so activations stay
-O(1) through 16-36 blocks.  Tolerances: fp32 mode |dlogit| <= 1e-3 (the
-north-star bar); bf16 mode pooled features relative error <= 1e-1 (reported,
-not the parity gate).  parity pinned only through the oracle (no reference
+O(1) through 16-33 blocks.  Tolerances: fp32 mode |dlogit| <= 1e-3 (the
+north-star bar); bf16 mode pooled features relative error <= 5e-2 / 1e-1 / 2e-1
+for resnet34 / 50 / 101 (reported, not the parity gate).  parity pinned only through the oracle (no reference
 fixture exists for these backbones)."""
 import numpy as np
 import pytest
@@ -45,7 +45,7 @@ def maps(golden_frontend):
     return torch.from_numpy(golden_frontend['std_map'][:3]).contiguous()
 
 
-@pytest.mark.parametrize('name', ['resnet50', 'resnet34'])
+@pytest.mark.parametrize('name', ['resnet50', 'resnet34', 'resnet101'])
 def test_deep_resnet_vs_oracle(name, maps):
     from sad.engine import Engine, ResNetBackbone
     sd, ref, ref_feats = _calibrated(name, maps)
@@ -65,7 +65,9 @@ def test_deep_resnet_vs_oracle(name, maps):
     torch.cuda.synchronize()
     e16 = ((f16.cpu() - ref_feats).abs().max() / ref_feats.abs().max()).item()
     print(f'{name} bf16: pooled rel err {e16:.3e}')
-    assert e16 <= 1e-1
+    # bf16 noise grows with depth (resnet50: the CPU emulation of the bf16
+    # arithmetic is itself 6.9e-2 off, test_resnet50_bf16_vs_emulated_oracle)
+    assert e16 <= {'resnet34': 5e-2, 'resnet50': 1e-1, 'resnet101': 2e-1}[name]
 
 
 def test_deep_resnet_image_entry_matches_map_entry(maps):
