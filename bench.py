@@ -77,7 +77,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=2048, help='segments per GPU per step')
     ap.add_argument('--heads', type=int, default=6)
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'bf16x3', 'fp32'])
     ap.add_argument('--micro-batch', type=int, default=512,
                     help='segments per backbone launch sequence (stem/layer1/layer2 run in sub-batches of '
                          'SAD_FRONT_MB=32, layer3/4 on the whole micro-batch)')

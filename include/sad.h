@@ -43,6 +43,10 @@ enum sad_status {
 enum sad_dtype {
   SAD_F32 = 0,   /* fp32 activations, f32 MFMA (v_mfma_f32_16x16x4_f32): parity mode */
   SAD_BF16 = 1,  /* bf16 activations, bf16 MFMA (v_mfma_f32_16x16x32_bf16), f32 accumulate */
+  SAD_BF16X3 = 2 /* split-bf16 parity mode: every value v stored as hi = bf16(v), lo = bf16(v - hi)
+                    (channels interleaved [hi 32 | lo 32] per group of 32, 4 B per value like fp32);
+                    each product = W_hi.X_hi + W_lo.X_hi + W_hi.X_lo on bf16 MFMA, f32 accumulate:
+                    ~2^-17 relative operands, 3x the bf16 MFMA work, 16/3 x the f32 MFMA rate */
 };
 
 /* ---------------------------------------------------------------- runtime */

@@ -106,7 +106,27 @@ void fold_bn(const float* g, const float* beta, const float* mu, const float* va
   }
 }
 
-int upload_typed(void** dst, const std::vector<double>& v, int dtype) {
+int upload_typed(void** dst, const std::vector<double>& v, int dtype, int64_t row_len) {
+  if (dtype == SAD_BF16X3) {
+    // split-bf16: each row's K axis in groups of 32 -> [hi 32 | lo 32] (the
+    // activations' channel interleave, so one 128-B K-step pairs them up)
+    if (row_len <= 0 || row_len % 32 != 0 || v.size() % (size_t)row_len != 0) {
+      set_error("split-bf16 weights need rows of a multiple of 32 elements");
+      return SAD_ERR_ARG;
+    }
+    std::vector<u16> h(2 * v.size());
+    for (size_t i = 0; i < v.size(); ++i) {
+      const float x = (float)v[i];
+      const u16 hi = f2bf_host(x);
+      float hf;
+      const uint32_t hb = (uint32_t)hi << 16;
+      memcpy(&hf, &hb, 4);
+      const size_t g = i / 32, e = i % 32;
+      h[g * 64 + e] = hi;
+      h[g * 64 + 32 + e] = f2bf_host(x - hf);
+    }
+    return upload(dst, h);
+  }
   if (dtype == SAD_BF16) {
     std::vector<u16> h(v.size());
     for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_host((float)v[i]);
@@ -124,19 +144,33 @@ int fold_stem(const float* const* params, int dtype, void** w_out, float** b_out
   std::vector<double> sc, sh;
   fold_bn(params[1], params[2], params[3], params[4], 64, sc, sh);
   std::vector<double> w(64 * 64, 0.0);
+  const int wdt = dtype == SAD_BF16X3 ? SAD_BF16 : dtype;  // split stem: bf16 layout, hi then lo
   std::vector<float> b(64);
   for (int co = 0; co < 64; ++co) {
     for (int k = 0; k < 49; ++k) {
       double s = 0.0;
       for (int c = 0; c < 3; ++c) s += (double)W[(co * 3 + c) * 49 + k];
       // bf16 stem: (ky, kx) on an 8x8 grid; f32 stem: k = ky*7+kx, k=4q+g at g*16+q
-      const int pos = dtype == SAD_BF16 ? (k / 7) * 8 + (k % 7) : ((k & 3) * 16 + (k >> 2));
+      const int pos = wdt == SAD_BF16 ? (k / 7) * 8 + (k % 7) : ((k & 3) * 16 + (k >> 2));
       w[co * 64 + pos] = s * sc[co];
     }
     b[co] = (float)sh[co];
   }
   int rc;
-  if ((rc = upload_typed(w_out, w, dtype))) return rc;
+  if (dtype == SAD_BF16X3) {  // [64 co][64 k] hi, then [64][64] lo
+    std::vector<u16> h(2 * 64 * 64);
+    for (int i = 0; i < 64 * 64; ++i) {
+      const float x = (float)w[i];
+      h[i] = f2bf_host(x);
+      float hf;
+      const uint32_t hb = (uint32_t)h[i] << 16;
+      memcpy(&hf, &hb, 4);
+      h[64 * 64 + i] = f2bf_host(x - hf);
+    }
+    if ((rc = upload(w_out, h))) return rc;
+  } else if ((rc = upload_typed(w_out, w, dtype))) {
+    return rc;
+  }
   return upload((void**)b_out, b);
 }
 }  // namespace sad
@@ -146,7 +180,7 @@ extern "C" int sad_backbone_plan_create(const float* const* params, int32_t n_pa
   const std::vector<ConvSpec> specs = resnet18_specs();
   SAD_REQUIRE(params && out, "null params/out");
   SAD_REQUIRE(n_params == (int)specs.size() * 5, "n_params must be 100 (20 conv+BN groups)");
-  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
+  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16 || dtype == SAD_BF16X3, "dtype");
   SAD_REQUIRE(map_h > 0 && map_w > 0, "map shape");
   for (int i = 0; i < n_params; ++i) SAD_REQUIRE(params[i] != nullptr, "null parameter pointer");
   auto* p = new sad_backbone_plan();
@@ -157,7 +191,8 @@ extern "C" int sad_backbone_plan_create(const float* const* params, int32_t n_pa
   std::vector<double> sc, sh;
   int rc;
   if ((rc = fold_stem(params, dtype, &p->stem_w, &p->stem_b))) return rc;
-  for (size_t ci = 1; ci < specs.size(); ++ci) {
+  // first-generation per-conv weights (SAD_BACKBONE_PATH=igemm; fp32 / bf16 only)
+  for (size_t ci = 1; ci < specs.size() && dtype != SAD_BF16X3; ++ci) {
     const ConvSpec& s = specs[ci];
     const float* W = params[ci * 5];
     fold_bn(params[ci * 5 + 1], params[ci * 5 + 2], params[ci * 5 + 3], params[ci * 5 + 4], s.cout, sc, sh);
@@ -179,7 +214,7 @@ extern "C" int sad_backbone_plan_create(const float* const* params, int32_t n_pa
   // GEMM with a concatenated K axis; biases add.
   {
     const char* env = getenv("SAD_BACKBONE_PATH");
-    p->block_path = !(env && strcmp(env, "igemm") == 0);
+    p->block_path = !(env && strcmp(env, "igemm") == 0) || dtype == SAD_BF16X3;
     size_t ci = 1;
     int inp = 64;
     const int planes[4] = {64, 128, 256, 512};
@@ -216,8 +251,8 @@ extern "C" int sad_backbone_plan_create(const float* const* params, int32_t n_pa
             b2[o] = sh2[o];
           }
         }
-        if ((rc = upload_typed(&blk.w1, w1, dtype))) return rc;
-        if ((rc = upload_typed(&blk.w2, w2, dtype))) return rc;
+        if ((rc = upload_typed(&blk.w1, w1, dtype, k1))) return rc;
+        if ((rc = upload_typed(&blk.w2, w2, dtype, k2))) return rc;
         std::vector<float> b1f(sh1.begin(), sh1.end()), b2f(b2.begin(), b2.end());
         if ((rc = upload((void**)&blk.b1, b1f))) return rc;
         if ((rc = upload((void**)&blk.b2, b2f))) return rc;
@@ -250,7 +285,7 @@ extern "C" int sad_backbone_plan_destroy(sad_backbone_plan* p) {
 
 static constexpr int64_t kMaxActElems = 128ll * 128 * 64;  // per segment, layer1 map
 static size_t act_bytes(const sad_backbone_plan* p, int64_t mb) {
-  const size_t es = p->dtype == SAD_BF16 ? 2 : 4;
+  const size_t es = p->dtype == SAD_BF16 ? 2 : 4;  // fp32 and split-bf16: 4 B per value
   return ((size_t)mb * kMaxActElems * es + 255) & ~(size_t)255;
 }
 
@@ -788,7 +823,7 @@ extern "C" int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t
                                   int32_t variant, void* stream) {
   SAD_REQUIRE(in0 && wt && bias && out, "null tensor");
   SAD_REQUIRE(N >= 0 && H > 0 && W > 0 && k > 0 && stride > 0 && pad >= 0, "bad shape");
-  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
+  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16 || dtype == SAD_BF16X3, "dtype");
   BlockConvArgs a{};
   a.in0 = in0;
   a.in0_pstride = Cin;

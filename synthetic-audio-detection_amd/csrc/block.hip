@@ -61,9 +61,18 @@ constexpr int block_smem_bytes() {
 // RES: the epilogue adds a residual tensor (a Bottleneck's identity shortcut,
 // resnet.hip) -- its own instantiation, so the ResNet-18 kernels' register
 // allocation does not carry its loads
-template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES>
+// X3: split-bf16 parity mode (SAD_BF16X3).  Every tensor stores a logical fp32
+// value v as hi = bf16(v), lo = bf16(v - hi), channels interleaved in groups of
+// 32: [hi c0..31 | lo c0..31 | hi c32..63 | ...], so one 128-B K-step holds 32
+// logical channels, half 0 = hi, half 1 = lo, for pixels and weights alike.  A
+// K-step then runs three MFMA sets, W_hi.X_hi + W_lo.X_hi + W_hi.X_lo (the
+// dropped W_lo.X_lo is ~2^-18 relative), accumulated in fp32; the epilogue
+// splits the fp32 result again.  An identity shortcut (W_hi = I, W_lo = 0)
+// adds X_hi + X_lo exactly.
+template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES, bool X3 = false>
 __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_kernel(BlockConvArgs a) {
   static_assert(S == 2 || S == 3, "ring depth");
+  static_assert(!X3 || sizeof(T) == 2, "split-bf16 operands are bf16");
   constexpr int NW = WC * WP;
   constexpr int BC = 16 * TC * WC, BP = 16 * TP * WP;  // channels x pixels per tile
   constexpr int ES = sizeof(T);
@@ -239,22 +248,26 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
       for (int i = 0; i < TC; ++i) {
 #pragma unroll
         for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pf[j], acc[i][j]);
+        if constexpr (X3) {  // W_hi . X_lo while W_hi is still in registers
+#pragma unroll
+          for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pg[j], acc[i][j]);
+        }
         const int r = BP + wc * 16 * TC + i * 16 + fr;
         wf[i] = *(const uint4*)(base + r * 128 + (swz(r, fg + 4) << 4));
       }
-      // order: half 1's pixel reads, then per weight row i its TP MFMAs followed
-      // by the read of its half-1 fragment
+      // order: half 1's pixel reads, then per weight row i its TP (X3: 2 TP)
+      // MFMAs followed by the read of its half-1 fragment
       __builtin_amdgcn_sched_group_barrier(0x100, TP, 0);
 #pragma unroll
       for (int i = 0; i < TC; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, TP, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, X3 ? 2 * TP : TP, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < TC; ++i)
 #pragma unroll
-        for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pg[j], acc[i][j]);
+        for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], X3 ? pf[j] : pg[j], acc[i][j]);  // X3: W_lo . X_hi
     } else {
     if (do_issue) issue(ist);
     // both K-halves' fragments in registers; half 1's reads are issued between
@@ -275,19 +288,35 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
         pf[s][j] = *(const uint4*)(base + r * 128 + (swz(r, c) << 4));
       }
     }
+if constexpr (X3) {
+      static_assert(!X3 || TC * TP >= TC + TP, "X3 schedule needs TC*TP >= TC+TP");
+      // W_hi.X_hi first (half 0 only), then W_lo.X_hi and W_hi.X_lo
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[0][i], pf[0][j], acc[i][j]);
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) {
+          mfma_chunk<T>(wf[1][i], pf[0][j], acc[i][j]);
+          mfma_chunk<T>(wf[0][i], pf[1][j], acc[i][j]);
+        }
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < TC; ++i)
 #pragma unroll
         for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[s][i], pf[s][j], acc[i][j]);
+    }
     __builtin_amdgcn_sched_group_barrier(0x100, TC + TP, 0);
 #pragma unroll
     for (int k = 0; k < TC + TP; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * TC * TP - (TC + TP), 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, (X3 ? 3 : 2) * TC * TP - (TC + TP), 0);
     }
     st = st + 1 == S ? 0 : st + 1;
     if (++cks == nk) {
@@ -341,11 +370,16 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
           // compiler cannot move a load above a store that may alias it, so
           // interleaved loads would each wait for the stores before them)
           using RV = typename std::conditional<sizeof(T) == 2, uint2, float4>::type;
-          RV rres[RES ? TC : 1];
+          RV rres[RES ? TC : 1], rlo[RES && X3 ? TC : 1];
           if constexpr (RES) {
-            const T* rp = (const T*)a.res + (int64_t)px * a.res_pstride + c0 + wc * 16 * TC + fg * 4;
+            const T* rp = (const T*)a.res + (int64_t)px * a.res_pstride;
 #pragma unroll
-            for (int i = 0; i < TC; ++i) rres[i] = *(const RV*)(rp + i * 16);
+            for (int i = 0; i < TC; ++i) {
+              const int co = c0 + wc * 16 * TC + i * 16 + fg * 4;
+              const int pc = X3 ? ((co >> 5) << 6) + (co & 31) : co;  // split layout: hi at pc, lo at pc + 32
+              rres[i] = *(const RV*)(rp + pc);
+              if constexpr (X3) rlo[i] = *(const RV*)(rp + pc + 32);
+            }
           }
 #pragma unroll
           for (int i = 0; i < TC; ++i) {
@@ -362,10 +396,18 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
             if constexpr (RES) {
               if constexpr (sizeof(T) == 2) {
                 const uint2 q = rres[i];
-                v[0] += bf2f((u16)(q.x & 0xFFFF));
-                v[1] += bf2f((u16)(q.x >> 16));
-                v[2] += bf2f((u16)(q.y & 0xFFFF));
-                v[3] += bf2f((u16)(q.y >> 16));
+                if constexpr (X3) {
+                  const uint2 l = rlo[i];
+                  v[0] += bf2f((u16)(q.x & 0xFFFF)) + bf2f((u16)(l.x & 0xFFFF));
+                  v[1] += bf2f((u16)(q.x >> 16)) + bf2f((u16)(l.x >> 16));
+                  v[2] += bf2f((u16)(q.y & 0xFFFF)) + bf2f((u16)(l.y & 0xFFFF));
+                  v[3] += bf2f((u16)(q.y >> 16)) + bf2f((u16)(l.y >> 16));
+                } else {
+                  v[0] += bf2f((u16)(q.x & 0xFFFF));
+                  v[1] += bf2f((u16)(q.x >> 16));
+                  v[2] += bf2f((u16)(q.y & 0xFFFF));
+                  v[3] += bf2f((u16)(q.y >> 16));
+                }
               } else {
                 const float4 q = rres[i];
                 v[0] += q.x;
@@ -376,6 +418,19 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 if (a.relu) v[r] = fmaxf(v[r], 0.f);
+            }
+            if constexpr (X3) {
+              T* op = out + (int64_t)px * a.out_pstride + ((co >> 5) << 6) + (co & 31);
+              u16 h[4], l[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                h[r] = f2bf(v[r]);
+                l[r] = f2bf(v[r] - bf2f(h[r]));
+              }
+              *(uint2*)op = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+              *(uint2*)(op + 32) =
+                  make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
+              continue;
             }
             T* op = out + (int64_t)px * a.out_pstride + co;
             if constexpr (sizeof(T) == 2) {
@@ -399,14 +454,14 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES_OK = false>
+template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES_OK = false, bool X3 = false>
 static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
   constexpr int smem = block_smem_bytes<WC, WP, TC, TP, S, OCC>();
   static_assert(smem * OCC <= 160 * 1024, "LDS budget");
   SAD_REQUIRE(RES_OK || !a.res, "this block-conv variant has no epilogue residual (variants 13, 20, 21, 25 do)");
-  const void* kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false>;
+  const void* kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3>;
   if constexpr (RES_OK) {
-    if (a.res) kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true>;
+    if (a.res) kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true, X3>;
   }
   static bool attr[2] = {false, false};
   if (!attr[a.res != nullptr]) {
@@ -430,17 +485,17 @@ static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
               "block conv: too many pixels for one launch (lower the micro-batch)");
   if constexpr (RES_OK) {
     if (a.res) {
-      hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true>), dim3((unsigned)g), dim3(64 * WC * WP),
-                         smem, s, a);
+      hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true, X3>), dim3((unsigned)g),
+                         dim3(64 * WC * WP), smem, s, a);
       SAD_CHECK_HIP(hipGetLastError());
       return SAD_OK;
     }
   }
-  hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false>), dim3((unsigned)g), dim3(64 * WC * WP), smem, s, a);
+  hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3>), dim3((unsigned)g), dim3(64 * WC * WP),
+                     smem, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }
-
 
 // Variants (channels x pixels tile, waves, wave tile, ring stages, LDS, workgroups/CU):
 //  9: 64x256  4w 64x64  S2  80 KB 2     10: 128x128 4w 64x64  S2  64 KB 2
@@ -448,19 +503,19 @@ static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
 // 13: 256x256 8w 128x64 S2 128 KB 1     14: 128x256 8w 64x64  S2  96 KB 1
 // 15: 128x256 8w 64x64  S3 144 KB 1     16: 64x512  8w 64x64  S2 144 KB 1
 // 17: 256x128 4w 128x64 S2  96 KB 1     18: 128x256 4w 64x128 S2  96 KB 1
-template <typename T>
+template <typename T, bool X3 = false>
 static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
   switch (v) {
-    case 9: return launch_block_t<T, 1, 4, 4, 4, 2, 2>(a, s);
-    case 10: return launch_block_t<T, 2, 2, 4, 4, 2, 2>(a, s);
-    case 11: return launch_block_t<T, 1, 4, 4, 4, 3, 1>(a, s);
-    case 12: return launch_block_t<T, 2, 2, 4, 4, 3, 1>(a, s);
-    case 13: return launch_block_t<T, 2, 4, 8, 4, 2, 1, true>(a, s);
-    case 14: return launch_block_t<T, 2, 4, 4, 4, 2, 1>(a, s);
-    case 15: return launch_block_t<T, 2, 4, 4, 4, 3, 1>(a, s);
-    case 16: return launch_block_t<T, 1, 8, 4, 4, 2, 1>(a, s);
-    case 17: return launch_block_t<T, 2, 2, 8, 4, 2, 1>(a, s);
-    case 18: return launch_block_t<T, 2, 2, 4, 8, 2, 1>(a, s);
+    case 9: return launch_block_t<T, 1, 4, 4, 4, 2, 2, false, X3>(a, s);
+    case 10: return launch_block_t<T, 2, 2, 4, 4, 2, 2, false, X3>(a, s);
+    case 11: return launch_block_t<T, 1, 4, 4, 4, 3, 1, false, X3>(a, s);
+    case 12: return launch_block_t<T, 2, 2, 4, 4, 3, 1, false, X3>(a, s);
+    case 13: return launch_block_t<T, 2, 4, 8, 4, 2, 1, true, X3>(a, s);
+    case 14: return launch_block_t<T, 2, 4, 4, 4, 2, 1, false, X3>(a, s);
+    case 15: return launch_block_t<T, 2, 4, 4, 4, 3, 1, false, X3>(a, s);
+    case 16: return launch_block_t<T, 1, 8, 4, 4, 2, 1, false, X3>(a, s);
+    case 17: return launch_block_t<T, 2, 2, 8, 4, 2, 1, false, X3>(a, s);
+    case 18: return launch_block_t<T, 2, 2, 4, 8, 2, 1, false, X3>(a, s);
   }
   set_error("unknown block-conv variant");
   return SAD_ERR_ARG;
@@ -523,8 +578,21 @@ static bool variant_fits(int v, int cout) {
 }
 
 int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int variant) {
-  const int ES = dtype == SAD_BF16 ? 2 : 4;
+  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16 || dtype == SAD_BF16X3, "dtype");
+  const int ES = dtype == SAD_F32 ? 4 : 2;
   BlockConvArgs a = a_in;
+  if (dtype == SAD_BF16X3) {
+    // callers count logical channels; the kernel sees the split layout's bf16
+    // channels (2 per logical channel, hi/lo interleaved in groups of 32)
+    SAD_REQUIRE(a.Cin % 32 == 0 && a.Cin1 % 32 == 0, "split-bf16: channels must be multiples of 32");
+    a.Cin *= 2;
+    a.Cin1 *= 2;
+    a.in0_pstride *= 2;
+    a.in1_pstride *= 2;
+    a.out_pstride *= 2;
+    a.res_pstride *= 2;
+    a.wt_ld *= 2;
+  }
   a.in0_bytes = (((int64_t)a.N * a.H * a.W - 1) * a.in0_pstride + a.Cin) * ES;
   a.in1_bytes = a.in1 ? (((int64_t)a.N * a.H1 * a.W1 - 1) * a.in1_pstride + a.Cin1) * ES : 0;
   if (a.wt_ld == 0) a.wt_ld = a.KH * a.KW * a.Cin + (a.in1 ? a.Cin1 : 0);
@@ -550,6 +618,10 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
     return launch_halo_v(a, v, s);
   }
   SAD_REQUIRE(!a.res || a.res_pstride % 4 == 0, "residual pixel stride must keep 4-channel alignment");
+  if (dtype == SAD_BF16X3) {
+    SAD_REQUIRE(v >= 9 && v <= 18, "split-bf16 runs on the implicit-GEMM variants 9..18");
+    return launch_block_v<u16, true>(a, v, s);
+  }
   return dtype == SAD_BF16 ? launch_block_v<u16>(a, v, s) : launch_block_v<float>(a, v, s);
 }
 

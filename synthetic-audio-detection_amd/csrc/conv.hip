@@ -466,15 +466,31 @@ __device__ __forceinline__ float dppf(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
-__global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
+// X3 (split-bf16 parity mode, SAD_BF16X3): the band is kept as hi and lo bf16
+// planes, the weights as hi and lo, each product is W_hi.X_hi + W_lo.X_hi +
+// W_hi.X_lo, and the pooled output is stored split ([hi 32 | lo 32] per 32
+// channels; one workgroup per CU for the larger LDS footprint).
+constexpr int STEM_OPITCH_X3 = 288;  // 128 bf16 (64 ch hi + lo) + pad: 72 dwords -> 4 rows on disjoint bank sets
+template <bool X3>
+constexpr int stem_u_floats() {
+  return X3 ? (128 * STEM_OPITCH_X3 / 4 + 256 > STEM_HROWS * 512 + 256 ? 128 * STEM_OPITCH_X3 / 4 + 256
+                                                                         : STEM_HROWS * 512 + 256)
+            : STEM_HROWS * 512 + 256;
+}
+
+template <bool X3>
+__global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) {
+  constexpr int OPITCH = X3 ? STEM_OPITCH_X3 : STEM_OPITCH;
   __shared__ __attribute__((aligned(16))) u16 s_img[STEM_BAND_ROWS * STEM_BPITCH];
+  __shared__ __attribute__((aligned(16))) u16 s_imgl[X3 ? STEM_BAND_ROWS * STEM_BPITCH : 8];
   __shared__ __attribute__((aligned(16))) u16 s_w[64 * 72];
+  __shared__ __attribute__((aligned(16))) u16 s_wl[X3 ? 64 * 72 : 8];
   __shared__ __attribute__((aligned(16))) float s_bias[64];
   // x-interpolated map rows while the band is built; afterwards the pooled-row
-  // staging [128 q][64 ch] bf16 and the wave-edge exchange [4][64] fp32
-  __shared__ __attribute__((aligned(16))) float s_u[STEM_HROWS * 512 + 256];
-  char* s_out = (char*)s_u;                  // pooled row staging, [128 q][STEM_OPITCH B]
-  float* s_edge = s_u + 128 * STEM_OPITCH / 4;  // [4 waves][64 ch]
+  // staging [128 q][64 ch] bf16 (X3: hi + lo) and the wave-edge exchange [4][64] fp32
+  __shared__ __attribute__((aligned(16))) float s_u[stem_u_floats<X3>()];
+  char* s_out = (char*)s_u;                  // pooled row staging, [128 q][OPITCH B]
+  float* s_edge = s_u + 128 * OPITCH / 4;    // [4 waves][64 ch]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int py0 = blockIdx.x * STEM_P;
@@ -482,7 +498,14 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
   for (int i = tid; i < 64 * 8; i += 256) {  // [64 co][64 k] bf16 -> pitch 72
     const int co = i >> 3, c8 = (i & 7) * 8;
     *(uint4*)(s_w + co * 72 + c8) = *(const uint4*)((const u16*)a.w + co * 64 + c8);
+    if constexpr (X3) *(uint4*)(s_wl + co * 72 + c8) = *(const uint4*)((const u16*)a.w + 64 * 64 + co * 64 + c8);
   }
+  // band element store: bf16, or the hi/lo pair
+  auto put = [&](int i, float v) __attribute__((always_inline)) {
+    const u16 h = f2bf(v);
+    s_img[i] = h;
+    if constexpr (X3) s_imgl[i] = f2bf(v - bf2f(h));
+  };
   if (tid < 64) s_bias[tid] = a.bias[tid];
   // ---- image band: rows iy = 4*py0 - 5 + tr, cols ix = tc - 3 (zero outside 512x512)
   // every band row a fragment reads, incl. the zero-weight tap row ky = 7
@@ -494,7 +517,7 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
       const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
       float v = 0.f;
       if ((unsigned)iy < 512u && (unsigned)ix < 512u) v = a.img[(b * 512 + iy) * 512 + ix];
-      s_img[i] = f2bf(v);
+      put(i, v);
     }
   } else {
     const float* __restrict__ map = a.map + b * a.mh * a.mw;
@@ -555,7 +578,7 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
           src_row(iy, y0, y1, ly);
           v = (1.f - ly) * s_u[(y0 - ylo) * 512 + ix] + ly * s_u[(y1 - ylo) * 512 + ix];
         }
-        s_img[i] = f2bf(v);
+        put(i, v);
       }
     } else {  // very tall maps: direct bilinear per pixel
       for (int i = tid; i < NBR * STEM_BPITCH; i += 256) {
@@ -563,7 +586,7 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
         const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
         float v = 0.f;
         if ((unsigned)iy < 512u && (unsigned)ix < 512u) v = bilinear512(map, a.mh, a.mw, sh, sw, iy, ix);
-        s_img[i] = f2bf(v);
+        put(i, v);
       }
     }
   }
@@ -586,16 +609,21 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
       for (int j = 0; j < 4; ++j) r[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int rb = 2 * (cr - 2 * py0) + 2;
     uint4 bw[4][2];  // weight fragments (LDS-resident; re-read per row keeps VGPRs for the pool)
+    uint4 bwl[X3 ? 4 : 1][2];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) bw[j][s] = *(const uint4*)(s_w + (j * 16 + fr) * 72 + 32 * s + 8 * fg);
+      for (int s = 0; s < 2; ++s) {
+        bw[j][s] = *(const uint4*)(s_w + (j * 16 + fr) * 72 + 32 * s + 8 * fg);
+        if constexpr (X3) bwl[j][s] = *(const uint4*)(s_wl + (j * 16 + fr) * 72 + 32 * s + 8 * fg);
+      }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int cx = wave * 64 + i * 16 + fr;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const u16* p = s_img + (rb + 4 * s + fg) * STEM_BPITCH + 2 * cx;
+        const int o = (rb + 4 * s + fg) * STEM_BPITCH + 2 * cx;
+        const u16* p = s_img + o;
         uint4 av;
         av.x = *(const uint32_t*)(p + 0);
         av.y = *(const uint32_t*)(p + 2);
@@ -603,6 +631,19 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
         av.w = *(const uint32_t*)(p + 6);
 #pragma unroll
         for (int j = 0; j < 4; ++j) mfma_chunk<u16>(av, bw[j][s], r[i][j]);  // C[px][ch]
+        if constexpr (X3) {
+          const u16* pl = s_imgl + o;
+          uint4 al;
+          al.x = *(const uint32_t*)(pl + 0);
+          al.y = *(const uint32_t*)(pl + 2);
+          al.z = *(const uint32_t*)(pl + 4);
+          al.w = *(const uint32_t*)(pl + 6);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            mfma_chunk<u16>(av, bwl[j][s], r[i][j]);  // X_hi . W_lo
+            mfma_chunk<u16>(al, bw[j][s], r[i][j]);   // X_lo . W_hi
+          }
+        }
       }
     }
   };
@@ -655,18 +696,28 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
         const float ob = fmaxf(fmaxf(fmaxf(x[1], x[2]), x[3]) + bias[j], 0.f);
         const float oa_next = dppf<0x101>(oa);  // row_shl:1 (fr + 1)
         const float ob_prev = dppf<0x111>(ob);  // row_shr:1 (fr - 1)
-        const float lo = even ? oa : ob_prev, hi = even ? oa_next : ob;
+        // c0 = channel fr & ~1 (value v0), c0 + 1 (value v1) of pooled pixel q
+        const float v0 = even ? oa : ob_prev, v1 = even ? oa_next : ob;
         const int q = wave * 32 + i * 8 + 2 * fg + (even ? 0 : 1);
-        *(uint32_t*)(s_out + q * STEM_OPITCH + (j * 16 + (fr & ~1)) * 2) =
-            (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+        const int c0 = j * 16 + (fr & ~1);
+        const u16 h0 = f2bf(v0), h1 = f2bf(v1);
+        if constexpr (X3) {
+          const int pc = ((c0 >> 5) << 6) + (c0 & 31);
+          *(uint32_t*)(s_out + q * OPITCH + pc * 2) = (uint32_t)h0 | ((uint32_t)h1 << 16);
+          *(uint32_t*)(s_out + q * OPITCH + pc * 2 + 64) =
+              (uint32_t)f2bf(v0 - bf2f(h0)) | ((uint32_t)f2bf(v1 - bf2f(h1)) << 16);
+        } else {
+          *(uint32_t*)(s_out + q * OPITCH + c0 * 2) = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        }
       }
     }
     __syncthreads();
-    u16* __restrict__ out = (u16*)a.out + ((b * 128 + py) * 128) * 64;
+    constexpr int PXE = X3 ? 128 : 64;  // bf16 elements per pooled pixel
+    u16* __restrict__ out = (u16*)a.out + ((b * 128 + py) * 128) * PXE;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int idx = (k * 256 + tid) * 8;  // 16 KB row, 16 B per thread per k
-      *(uint4*)(out + idx) = *(const uint4*)(s_out + (idx >> 6) * STEM_OPITCH + (idx & 63) * 2);
+    for (int k = 0; k < PXE / 16; ++k) {
+      const int idx = (k * 256 + tid) * 8;  // 16 (X3: 32) KB row, 16 B per thread per k
+      *(uint4*)(out + idx) = *(const uint4*)(s_out + (idx / PXE) * OPITCH + (idx % PXE) * 2);
     }
     __syncthreads();
   }
@@ -675,16 +726,21 @@ __global__ __launch_bounds__(256, 2) void stem_bf16_kernel(StemArgs a) {
 // --------------------------------------------------------------- avgpool --
 // [B, HW, C] (NHWC, dtype T) -> [B, C] fp32 mean over HW.  Workgroup = one
 // segment x 64 channels; 4 waves split the pixels, LDS combine.
-template <typename T>
+// X3: split-bf16 input ([hi 32 | lo 32] per 32 channels, 2c bf16 per pixel).
+template <typename T, bool X3 = false>
 __global__ __launch_bounds__(256) void avgpool_kernel(const T* __restrict__ in, int hw, int c,
                                                       float* __restrict__ out) {
   __shared__ float part[4][64];
   const int64_t b = blockIdx.x;
   const int ch = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
-  const T* p = in + b * hw * c + ch;
+  const int pc = X3 ? ((ch >> 5) << 6) + (ch & 31) : ch;
+  const int ps = X3 ? 2 * c : c;
+  const T* p = in + b * hw * ps + pc;
   float s = 0.f;
   for (int i = g; i < hw; i += 4) {
-    if constexpr (sizeof(T) == 2)
+    if constexpr (X3)
+      s += bf2f(p[(int64_t)i * ps]) + bf2f(p[(int64_t)i * ps + 32]);
+    else if constexpr (sizeof(T) == 2)
       s += bf2f(p[(int64_t)i * c]);
     else
       s += p[(int64_t)i * c];
@@ -762,7 +818,9 @@ int launch_stem(const StemArgs& a, int dtype, hipStream_t s) {
   SAD_REQUIRE(a.B <= 65535, "stem: B > 65535");
   if (a.B == 0) return SAD_OK;
   if (dtype == SAD_BF16)
-    hipLaunchKernelGGL(stem_bf16_kernel, dim3(128 / STEM_P, (unsigned)a.B), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(stem_bf16_kernel<false>, dim3(128 / STEM_P, (unsigned)a.B), dim3(256), 0, s, a);
+  else if (dtype == SAD_BF16X3)
+    hipLaunchKernelGGL(stem_bf16_kernel<true>, dim3(128 / STEM_P, (unsigned)a.B), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(stem_kernel<float>, dim3(128, (unsigned)a.B), dim3(256), 0, s, a);
   SAD_CHECK_HIP(hipGetLastError());
@@ -771,7 +829,10 @@ int launch_stem(const StemArgs& a, int dtype, hipStream_t s) {
 
 int launch_avgpool(const void* in, int64_t B, int hw, int c, float* out, int dtype, hipStream_t s) {
   if (B == 0) return SAD_OK;
-  if (dtype == SAD_BF16)
+  if (dtype == SAD_BF16X3)
+    hipLaunchKernelGGL((avgpool_kernel<u16, true>), dim3((unsigned)B, c / 64), dim3(256), 0, s, (const u16*)in, hw, c,
+                       out);
+  else if (dtype == SAD_BF16)
     hipLaunchKernelGGL(avgpool_kernel<u16>, dim3((unsigned)B, c / 64), dim3(256), 0, s, (const u16*)in, hw, c, out);
   else
     hipLaunchKernelGGL(avgpool_kernel<float>, dim3((unsigned)B, c / 64), dim3(256), 0, s, (const float*)in, hw, c, out);

@@ -87,7 +87,8 @@ int upload(void** dst, const std::vector<V>& v) {
 // BN (eval) as a per-channel affine: scale = g / sqrt(var + 1e-5), shift = beta - mu * scale
 void fold_bn(const float* g, const float* beta, const float* mu, const float* var, int c,
              std::vector<double>& scale, std::vector<double>& shift);
-int upload_typed(void** dst, const std::vector<double>& v, int dtype);  // fp32 or bf16 (RNE)
+// fp32, bf16 (RNE) or split-bf16 (row_len: K per weight row, hi/lo interleaved per 32)
+int upload_typed(void** dst, const std::vector<double>& v, int dtype, int64_t row_len = 0);
 // timm conv1 + bn1 (5 arrays) -> the stem kernel's weight layout and bias
 int fold_stem(const float* const* params, int dtype, void** w_out, float** b_out);
 

@@ -74,7 +74,7 @@ int fold_conv(const float* const* q, int cout, int cin, int k, int dtype, ConvW&
   out.k = k;
   out.ld = ld;
   int rc;
-  if ((rc = upload_typed(&out.w, w, dtype))) return rc;
+  if ((rc = upload_typed(&out.w, w, dtype, ld))) return rc;
   return upload((void**)&out.b, b);
 }
 
@@ -113,7 +113,7 @@ extern "C" int sad_resnet_plan_create(const float* const* params, int32_t n_para
                                       sad_resnet_plan** out) {
   SAD_REQUIRE(params && layers && out, "null args");
   SAD_REQUIRE(block == SAD_BASIC_BLOCK || block == SAD_BOTTLENECK, "block must be SAD_BASIC_BLOCK or SAD_BOTTLENECK");
-  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
+  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16 || dtype == SAD_BF16X3, "dtype");
   SAD_REQUIRE(map_h > 0 && map_w > 0, "map shape");
   const int exp = block == SAD_BOTTLENECK ? 4 : 1;
   const int per_block = block == SAD_BOTTLENECK ? 3 : 2;

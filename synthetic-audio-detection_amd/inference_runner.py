@@ -121,8 +121,8 @@ class ModularMultiHeadClassifier:
     @property
     def engine(self) -> _engine.Engine:
         if self._eng is None:
-            self._eng = _engine.Engine(self.state_dict(), self.device, dtype='bf16' if self.precision == 'bf16'
-                                       else 'fp32', micro_batch=self.micro_batch)
+            self._eng = _engine.Engine(self.state_dict(), self.device, dtype=self.precision,
+                                       micro_batch=self.micro_batch)
         return self._eng
 
     def to(self, device):
@@ -357,8 +357,9 @@ def main(argv=None):
     parser.add_argument('--confidence-threshold', type=float, default=0.45, help='Confidence threshold for segments.')
     parser.add_argument('--smooth', action='store_true', help='Apply smoothing across windows.')
     parser.add_argument('--output-json', type=str, default='results.json')
-    parser.add_argument('--precision', choices=['fp32', 'bf16'], default='fp32',
-                        help='device arithmetic: fp32 (reference numerics) or bf16 (throughput)')
+    parser.add_argument('--precision', choices=['fp32', 'bf16x3', 'bf16'], default='fp32',
+                        help='device arithmetic: fp32 (f32 MFMA), bf16x3 (split-bf16: logits within 1e-3 of fp32 '
+                             'at ~3x the fp32 speed) or bf16 (throughput; not logit-exact)')
     parser.add_argument('--batch-size', type=int, default=128, help='windows per device launch')
     parser.add_argument('--model-name', default='resnet18', choices=list(_weights.ARCHS),
                         help='backbone of the merged sub-models (the reference hard-codes resnet18, :77,246)')

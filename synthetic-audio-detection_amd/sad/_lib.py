@@ -20,6 +20,8 @@ LIB_PATH = os.environ.get('SAD_LIB', os.path.join(_HERE, 'libsad.so'))
 
 SAD_F32 = 0
 SAD_BF16 = 1
+SAD_BF16X3 = 2  # split-bf16 parity mode (include/sad.h)
+DTYPES = {'fp32': SAD_F32, 'bf16': SAD_BF16, 'bf16x3': SAD_BF16X3}
 
 # name -> (restype, argtypes); exactly the symbols include/sad.h declares.
 P = ctypes.c_void_p

@@ -83,10 +83,38 @@ class FrontEnd:
             pass
 
 
+def _dtype_code(dtype: str) -> int:
+    if dtype not in _lib.DTYPES:
+        raise ValueError(f'dtype must be one of {sorted(_lib.DTYPES)} (got {dtype!r})')
+    return _lib.DTYPES[dtype]
+
+
+def to_split(x: torch.Tensor) -> torch.Tensor:
+    """fp32 [..., C] -> the split-bf16 layout [..., 2C] bf16 of dtype 'bf16x3':
+    per group of 32 channels [hi(32) | lo(32)], hi = bf16(x), lo = bf16(x - hi)."""
+    C = x.shape[-1]
+    assert C % 32 == 0
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    g = torch.stack([hi.reshape(*x.shape[:-1], C // 32, 32), lo.reshape(*x.shape[:-1], C // 32, 32)], dim=-2)
+    return g.reshape(*x.shape[:-1], 2 * C).contiguous()
+
+
+def from_split(t: torch.Tensor) -> torch.Tensor:
+    """The split-bf16 layout [..., 2C] bf16 -> fp32 [..., C] (hi + lo)."""
+    C2 = t.shape[-1]
+    g = t.reshape(*t.shape[:-1], C2 // 64, 2, 32).float()
+    return (g[..., 0, :] + g[..., 1, :]).reshape(*t.shape[:-1], C2 // 2)
+
+
+def _act_channels(dtype: str, c: int) -> int:
+    return 2 * c if dtype == 'bf16x3' else c
+
+
 def resize(map_: torch.Tensor, size=(512, 512), dtype: str = 'fp32') -> torch.Tensor:
     """Device bilinear resize (torchvision Resize semantics) of [n, h, w] fp32."""
     n, h, w = map_.shape
-    dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
+    dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32  # resize output: fp32 or bf16 image
     out = torch.empty(n, size[0], size[1], device=map_.device,
                       dtype=torch.bfloat16 if dt == _lib.SAD_BF16 else torch.float32)
     with torch.cuda.device(map_.device):
@@ -102,8 +130,8 @@ class Backbone:
                  micro_batch: int = 64):
         self.device = _dev(device)
         self.dtype = dtype
-        self._dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
-        self.tdtype = torch.bfloat16 if dtype == 'bf16' else torch.float32
+        self._dt = _dtype_code(dtype)
+        self.tdtype = torch.float32 if dtype == 'fp32' else torch.bfloat16
         self.micro_batch = micro_batch
         arrays = []
         for key, _shape, kind in backbone_param_shapes():
@@ -151,23 +179,24 @@ class Backbone:
         return feats
 
     def stem(self, maps: torch.Tensor) -> torch.Tensor:
+        """NHWC [B,128,128,64] in the plan dtype (bf16x3: fp32 decoded from the split layout)."""
         B = maps.shape[0]
-        out = torch.empty(B, 128, 128, 64, device=self.device, dtype=self.tdtype)
+        out = torch.empty(B, 128, 128, _act_channels(self.dtype, 64), device=self.device, dtype=self.tdtype)
         with torch.cuda.device(self.device):
             _lib.call('sad_backbone_stem_run', self._plan, _lib.ptr(maps.contiguous()), B, _lib.ptr(out),
                       _lib.stream_handle(self.device))
-        return out
+        return from_split(out) if self.dtype == 'bf16x3' else out
 
     def debug(self, maps: torch.Tensor):
         """(pooled feats [B,512], layer4 map NHWC [B,16,16,512]) for small B."""
         B = maps.shape[0]
         feats = torch.empty(B, 512, device=self.device, dtype=torch.float32)
-        l4 = torch.empty(B, 16, 16, 512, device=self.device, dtype=self.tdtype)
+        l4 = torch.empty(B, 16, 16, _act_channels(self.dtype, 512), device=self.device, dtype=self.tdtype)
         ws = self.workspace(B)
         with torch.cuda.device(self.device):
             _lib.call('sad_backbone_run_debug', self._plan, _lib.ptr(maps.contiguous()), B, _lib.ptr(feats),
                       _lib.ptr(l4), _lib.ptr(ws), ws.numel(), _lib.stream_handle(self.device))
-        return feats, l4
+        return feats, (from_split(l4) if self.dtype == 'bf16x3' else l4)
 
     def __del__(self):
         try:
@@ -187,10 +216,10 @@ class ResNetBackbone:
         self.dtype = dtype
         self.model_name = model_name
         block, layers, self.num_features = arch_spec(model_name)
-        self._dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
+        self._dt = _dtype_code(dtype)
         # the widest activation (layer1 of a Bottleneck net: 128x128x256) must
         # stay under the kernels' 2 GiB buffer-addressing range
-        self.micro_batch = max(1, min(micro_batch, 128 if dtype == 'bf16' else 64))
+        self.micro_batch = max(1, min(micro_batch, 128 if dtype == 'bf16' else 64))  # fp32 / bf16x3: 4 B per value
         arrays = []
         for key, _shape, kind in arch_param_shapes(model_name):
             if kind == 'conv':
@@ -379,8 +408,10 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int = 1
 
 def block_conv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int = 1, pad: int = 1,
                sc: torch.Tensor | None = None, sc_stride: int = 1, relu: bool = True, variant: int = 0,
-               out: torch.Tensor | None = None, res: torch.Tensor | None = None, k: int = 3) -> torch.Tensor:
+               out: torch.Tensor | None = None, res: torch.Tensor | None = None, k: int = 3,
+               split: bool = False) -> torch.Tensor:
     """conv(x) + 1x1 shortcut(sc) [+ res] as ONE launch (libsad block-conv kernels).
+    split=True: every tensor in the split-bf16 layout (``to_split``; dtype 'bf16x3').
     x [N,H,W,Cin], sc [N,H1,W1,Cin1] or None, w [Cout, wt_ld] with the k*k*Cin
     conv taps first and the shortcut's Cin1 columns next (extra columns are
     ignored), bias [Cout] fp32, res [N,Ho,Wo,Cout] (epilogue identity shortcut)."""
@@ -389,11 +420,17 @@ def block_conv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int
     Cin1 = sc.shape[3] if sc is not None else 0
     Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
     dt = _lib.SAD_BF16 if x.dtype == torch.bfloat16 else _lib.SAD_F32
+    if split:  # x, sc, res, out, w in the split-bf16 layout; channel counts are logical
+        dt = _lib.SAD_BF16X3
+        Cin, Cin1, wt_ld = Cin // 2, Cin1 // 2, w.stride(0) // 2
+    else:
+        wt_ld = w.stride(0)
     if out is None:
-        out = torch.empty(N, Ho, Wo, Cout, device=x.device, dtype=x.dtype)
+        out = torch.empty(N, Ho, Wo, _act_channels('bf16x3' if split else 'bf16', Cout), device=x.device,
+                          dtype=x.dtype)
     H1, W1 = (sc.shape[1], sc.shape[2]) if sc is not None else (0, 0)
     with torch.cuda.device(x.device):
         _lib.call('sad_block_conv_run', _lib.ptr(x), N, H, W, Cin, _lib.ptr(sc), H1, W1, Cin1, sc_stride,
-                  _lib.ptr(w), w.stride(0), _lib.ptr(bias), _lib.ptr(res), _lib.ptr(out), Cout, k, stride, pad,
+                  _lib.ptr(w), wt_ld, _lib.ptr(bias), _lib.ptr(res), _lib.ptr(out), Cout, k, stride, pad,
                   int(relu), dt, variant, _lib.stream_handle(x.device))
     return out
