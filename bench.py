@@ -8,16 +8,27 @@ counter-hash PRNG, rank-disjoint ranges) -> fused STFT/mel/dB/standardise ->
 fused resize+stem -> ResNet-18 (bf16 MFMA implicit GEMM) -> 6 heads + merge ->
 RCCL all-gather of the merged logits to every rank (N > 1).  Weak scaling.
 
-Prints ONE JSON line on rank 0 (driver contract) with `roofline` (the dominant
-kernel, the 256x256 block-conv of layer3/4, MFMA-bound: algorithmic FLOPs of its
-launches in the last timed step over their HIP-event durations recorded by
-libsad on the launch stream; `traffic` from the committed PMC passes; the whole
-backbone's rate as `roofline.backbone`) and `cpu_baseline` (the CPU oracle in the
-reference's structure, on a bounded sample, rank 0 at N=1 only).
+``--gpus N`` without a launcher starts N ranks itself (sad/launch.py: a
+torch.distributed.run child); under a launcher the world size must equal N.
+
+Prints ONE JSON line on rank 0 (driver contract).  Besides the headline (bf16,
+configs[2]) it carries, measured in the same run on the same segments:
+  * ``parity_mode``: the split-bf16 mode (dtype bf16x3) that meets the
+    north-star |dlogit| <= 1e-3 -- its segments/s, roofline of its dominant
+    kernel, max|dlogit| against the reference-generated golden logits and
+    against the fp32 device path over the whole batch, decision agreement;
+  * ``accuracy``: the same numbers for the bf16 headline mode;
+  * ``fp32_mode``: the f32-MFMA mode's rate (N = 1);
+  * ``roofline`` (the dominant kernel, the 256x256 block-conv of layer3/4:
+    algorithmic FLOPs of its launches in the last timed step over their HIP
+    event durations recorded by libsad on the launch stream; ``traffic`` from
+    the committed PMC passes) and ``cpu_baseline`` (configs[0]: the CPU oracle
+    in the reference's structure on 64 synthetic WAV clips, rank 0 at N = 1).
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -28,183 +39,320 @@ sys.path[:0] = [ROOT, PKG]
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from sad import launch  # noqa: E402
+
 SEG = 128000
-# Algorithmic work per segment (DESIGN.md "Roofline accounting"):
+# Algorithmic work per segment:
 BACKBONE_FLOP = 18.13e9        # ResNet-18 @512^2 with conv1's 3 identical channels folded (reference: 18.95e9)
-REF_BACKBONE_FLOP = 18.95e9
-BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
-# The dominant kernel (36% of the step, profiles/r01_bench_kernels_final.md) and its
-# rocprof key in profiles/r01_pmc_traffic.json; 1344 TFLOP/s = the best bf16 GEMM
-# measured on this box (tools/gemm_ref.py)
+BF16_PEAK_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+F32_PEAK_TFLOPS = 157.3        # f32 MFMA = f32 vector peak (MI355X_MICROARCH.md)
+# The dominant kernel and its rocprof key in the committed PMC traffic file
 DOMINANT_VARIANT = 13
 DOMINANT_KERNEL = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1, false>|131072'
-# the same kernel's name in profiles taken before the epilogue-residual template flag (identical ISA)
 DOMINANT_KERNEL_OLD = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1>|131072'
-F32_PEAK_TFLOPS = 157.3
+TRAFFIC_JSON = os.path.join(ROOT, 'profiles', 'r01_pmc_traffic.json')
 FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats
 FE_BYTES = 256000 + 128512     # int16 PCM read + fp32 [128, 251] map written
+HEADS = 6
 
 
-def cpu_baseline(seconds: float = 15.0):
-    """The reference's CPU path (oracle restatement, fp32, torch CPU): per-window
-    front end, batch of up to 128 windows, ONE sub-model forward (configs[0])."""
+def cpu_model() -> str:
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or 'unknown'
+
+
+def cpu_baseline(n_clips: int = 64, passes: int = 2):
+    """configs[0]: the reference's CPU path (oracle restatement, fp32, torch CPU)
+    on 64 synthetic 4 s / 32 kHz WAV clips and ONE sub-model, in the
+    reference's structure: per-window front end (MelSpectrogram/AmplitudeToDB
+    rebuilt per call, standardise, Resize, repeat(3)), windows batched by 128,
+    the sub-model forward (inference_runner.py:144-174,276-289).  Timed twice:
+    from decoded fp32 waveforms in memory, and from the WAV files (decode +
+    mono + pad, preprocess_waveform :144-155, included)."""
+    import tempfile
+
     import numpy as np
     from oracle import frontend as ofe
     from oracle import resnet as ores
     from sad import weights as sw
+    from sad.audio import save_pcm16
     from sad.synth import synth_segment
+    import inference_runner as ir
     sd = sw.merged_state_dict(0, 1, False, bn_stats=sw.load_bn_stats(os.path.join(ROOT, 'tests', 'golden',
                                                                                     'bn_stats_n6.npz')))
     model = ores.load_merged_state(sd)
     cfg = ofe.SpectrogramConfig()
-    pcm = [torch.from_numpy(synth_segment(0, i).astype(np.float32) / 32768.0) for i in range(8)]
-    done, t0 = 0, time.perf_counter()
-    with torch.no_grad():
-        while time.perf_counter() - t0 < seconds:
-            specs = torch.cat([ofe.waveform_to_spectrogram(w, 32000, cfg) for w in pcm])
-            model(specs)
-            done += len(pcm)
-    dt = time.perf_counter() - t0
-    return {'value': done / dt, 'unit': 'segments/s', 'cores': torch.get_num_threads(), 'kind': 'port',
-            'sample': f'{done} synthetic 4 s segments in batches of 8 through the CPU oracle '
-                      f'(per-window mel/dB/std/resize + 1 sub-model ResNet-18, fp32), {dt:.1f} s'}
+    pcm = [synth_segment(0, i) for i in range(n_clips)]
+
+    def infer(waves):
+        with torch.no_grad():
+            for s in range(0, len(waves), 128):
+                specs = torch.cat([ofe.waveform_to_spectrogram(w, 32000, cfg) for w in waves[s:s + 128]])
+                model(specs)
+
+    waves = [torch.from_numpy(p.astype(np.float32) / 32768.0) for p in pcm]
+    infer(waves[:2])  # warm-up (allocator, thread pool)
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        infer(waves)
+    t_mem = time.perf_counter() - t0
+    with tempfile.TemporaryDirectory() as d:
+        paths = []
+        for i, p in enumerate(pcm):
+            paths.append(os.path.join(d, f'clip{i:03d}.wav'))
+            save_pcm16(paths[-1], p)
+        acfg = ir.AudioConfig()
+        t0 = time.perf_counter()
+        for _ in range(passes):
+            infer([ir.preprocess_waveform(p, acfg)[0] for p in paths])
+        t_wav = time.perf_counter() - t0
+    n = n_clips * passes
+    return {'value': round(n / t_mem, 2), 'unit': 'segments/s', 'cores': torch.get_num_threads(), 'kind': 'port',
+            'value_incl_wav_decode': round(n / t_wav, 2),
+            'host': {'os_cpu_count': os.cpu_count(), 'torch_threads': torch.get_num_threads(),
+                     'cpu_model': cpu_model()},
+            'sample': f'configs[0]: {n_clips} synthetic 4 s / 32 kHz clips x {passes} passes through the CPU '
+                      f'oracle (per-window mel/dB/std/resize/repeat(3), windows batched by 128, 1 sub-model '
+                      f'ResNet-18 + head, fp32): {t_mem:.1f} s from decoded waveforms; {t_wav:.1f} s from the WAV '
+                      f'files (decode, mono, pad included)'}
+
+
+class Mode:
+    """One engine configuration timed on this rank's resident PCM."""
+
+    def __init__(self, sd, dev, dtype, micro_batch, B, world):
+        from sad.engine import Engine
+        self.eng = Engine(sd, dev, dtype=dtype, micro_batch=micro_batch)
+        self.dtype, self.mb, self.B, self.world, self.dev = dtype, micro_batch, B, world, dev
+        self.feats = torch.empty(B, 512, device=dev)
+        self.logits = torch.empty(B, HEADS, 2, device=dev)
+        self.merged = torch.empty(B, HEADS + 1, device=dev)
+        self.gathered = torch.empty(world * B, HEADS + 1, device=dev) if world > 1 else None
+
+    def step(self, pcm, ev=None):
+        if ev is not None:
+            ev[0].record()
+        m = self.eng.frontend(pcm)
+        if ev is not None:
+            ev[1].record()
+        self.eng.backbones[0](m, out=self.feats)
+        if ev is not None:
+            ev[2].record()
+        self.eng.heads([self.feats], self.logits, self.merged)
+        if ev is not None:
+            ev[3].record()
+        if self.gathered is not None:
+            if dist.get_backend() == 'nccl':
+                dist.all_gather_into_tensor(self.gathered, self.merged)
+            else:  # gloo (the 2-rank one-GPU test)
+                dist.all_gather(list(self.gathered.chunk(self.world)), self.merged)
+        if ev is not None:
+            ev[4].record()
+
+    def run(self, pcm, steps, warmup, profile=True):
+        from sad import _lib
+        for _ in range(warmup):
+            self.step(pcm)
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(steps)]
+        t0 = time.perf_counter()
+        for i in range(steps):
+            if profile and i == steps - 1:
+                # HIP events around each block-conv launch of the last timed step,
+                # on its stream (events between launches cost ~5%, so one step only)
+                _lib.call('sad_profile_begin')
+            self.step(pcm, evs[i])
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        k_ms, k_n, k_fl = _lib.ctypes.c_double(), _lib.I64(), _lib.ctypes.c_double()
+        _lib.call('sad_profile_end', DOMINANT_VARIANT if profile else -1, _lib.ctypes.byref(k_ms),
+                  _lib.ctypes.byref(k_n), _lib.ctypes.byref(k_fl))
+        mean = lambda a, b: sum(e[a].elapsed_time(e[b]) for e in evs) / steps  # noqa: E731
+        r = {'elapsed': elapsed, 'fe_ms': mean(0, 1), 'bb_ms': mean(1, 2), 'heads_ms': mean(2, 3),
+             'gather_ms': mean(3, 4), 'k_ms': k_ms.value, 'k_n': k_n.value, 'k_flop': k_fl.value}
+        r['rank_ms_per_step'] = [round(elapsed * 1e3 / steps, 3)]
+        r['rank_gather_ms'] = [round(r['gather_ms'], 4)]
+        if self.world > 1:
+            t = torch.tensor([elapsed, r['gather_ms']], device=self.dev, dtype=torch.float64)
+            allt = [torch.empty_like(t) for _ in range(self.world)]
+            dist.all_gather(allt, t)
+            r['elapsed'] = max(x[0].item() for x in allt)
+            r['rank_ms_per_step'] = [round(x[0].item() * 1e3 / steps, 3) for x in allt]
+            r['rank_gather_ms'] = [round(x[1].item(), 4) for x in allt]
+        r['ms'] = r['elapsed'] * 1e3 / steps
+        r['value'] = self.world * self.B * steps / r['elapsed']
+        return r
+
+
+def kernel_roofline(r, mfma_factor=1):
+    """The dominant kernel's rate: algorithmic FLOPs / HIP-event time; the MFMA
+    work it executes is mfma_factor x that (split-bf16: 3 products per MAC)."""
+    n = max(r['k_n'], 1)
+    alg = r['k_flop'] / (r['k_ms'] * 1e-3) / 1e12 if r['k_ms'] > 0 else 0.0
+    return alg, alg * mfma_factor, {'launches': r['k_n'], 'launch_avg_us': round(r['k_ms'] * 1e3 / n, 2),
+                                    'flop_per_launch': round(r['k_flop'] / n)}
+
+
+def decisions(merged):
+    """Labels by the drop-in's interpret_multihead_logits (inference_runner.py:194-214)."""
+    import inference_runner as ir
+    names = [f'Synthetic{chr(65 + i)}' for i in range(HEADS)]
+    return [ir.interpret_multihead_logits(row, 0.5, names)[0] for row in merged.cpu()]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--steps', type=int, default=80)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=2048, help='segments per GPU per step')
-    ap.add_argument('--heads', type=int, default=6)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'bf16x3', 'fp32'])
-    ap.add_argument('--micro-batch', type=int, default=512,
-                    help='segments per backbone launch sequence (stem/layer1/layer2 run in sub-batches of '
-                         'SAD_FRONT_MB=32, layer3/4 on the whole micro-batch)')
+    ap.add_argument('--micro-batch', type=int, default=0,
+                    help='segments per backbone launch sequence (0: 512 bf16, 256 bf16x3, 128 fp32); stem/layer1 '
+                         'run in sub-batches of SAD_FRONT_MB=32, layers 2-4 on the whole micro-batch')
+    ap.add_argument('--parity-steps', type=int, default=0, help='timed steps of the bf16x3 parity mode '
+                                                                '(0: max(steps // 3, 3); -1: skip)')
+    ap.add_argument('--fp32-steps', type=int, default=2, help='timed steps of the fp32 mode (N = 1; 0: skip)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'], help='gloo: tests only')
+    ap.add_argument('--one-device', action='store_true', help='every rank on cuda:0 (2-rank test on one GPU)')
     args = ap.parse_args()
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+    if args.gpus > 1 and not launch.under_launcher():
+        sys.exit(launch.relaunch(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    world, rank, local = launch.check_world(args.gpus)
+    dev = torch.device('cuda', 0 if args.one_device else local)
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
 
+    import numpy as np
     from sad import _lib
     from sad import weights as sw
-    from sad.engine import Engine
-    stats = sw.load_bn_stats(os.path.join(ROOT, 'tests', 'golden', 'bn_stats_n6.npz'))
-    sd = sw.merged_state_dict(0, args.heads, False, bn_stats=stats)
-    eng = Engine(sd, dev, dtype=args.dtype, micro_batch=args.micro_batch)
+    gold = os.path.join(ROOT, 'tests', 'golden')
+    sd = sw.merged_state_dict(0, HEADS, False, bn_stats=sw.load_bn_stats(os.path.join(gold, 'bn_stats_n6.npz')))
+    mbs = {'bf16': 512, 'bf16x3': 256, 'fp32': 128}
     B = args.batch
     pcm = torch.empty(B, SEG, dtype=torch.int16, device=dev)
     _lib.call('sad_synth_pcm', 0, rank * B, B, SEG, _lib.ptr(pcm), _lib.stream_handle(dev))
-    maps = torch.empty(B, 128, 251, device=dev)
-    feats = torch.empty(B, 512, device=dev)
-    logits = torch.empty(B, args.heads, 2, device=dev)
-    merged = torch.empty(B, args.heads + 1, device=dev)
-    gathered = torch.empty(world * B, args.heads + 1, device=dev) if world > 1 else None
-    ev, fev = [], []
 
-    def step(timed):
-        if timed:
-            f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            f0.record()
-        m = eng.frontend(pcm)
-        if timed:
-            f1.record()
-            fev.append((f0, f1))
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        eng.backbones[0](m, out=feats)
-        if timed:
-            e1.record()
-            ev.append((e0, e1))
-        eng.heads([feats], logits, merged)
-        if gathered is not None:
-            dist.all_gather_into_tensor(gathered, merged)
+    head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world)
+    r = head.run(pcm, args.steps, args.warmup)
+    p_steps = max(args.steps // 3, 3) if args.parity_steps == 0 else args.parity_steps
+    par_mode, par = None, None
+    if p_steps > 0:
+        if args.dtype == 'bf16x3':
+            par_mode, par = head, r
+        else:
+            par_mode = Mode(sd, dev, 'bf16x3', mbs['bf16x3'], B, world)
+            par = par_mode.run(pcm, p_steps, 1)
 
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        if i == args.steps - 1:
-            # HIP events around each block-conv launch of the last timed step, on
-            # its stream (events between launches cost the step ~5%, so one step only)
-            _lib.call('sad_profile_begin')
-        step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    k_ms, k_n, k_fl = _lib.ctypes.c_double(), _lib.I64(), _lib.ctypes.c_double()
-    _lib.call('sad_profile_end', DOMINANT_VARIANT, _lib.ctypes.byref(k_ms), _lib.ctypes.byref(k_n),
-              _lib.ctypes.byref(k_fl))
-    bb_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
-    fe_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    ms = elapsed * 1e3 / args.steps
-    value = world * B * args.steps / elapsed
     if rank == 0:
-        peak = BF16_PEAK_TFLOPS if args.dtype == 'bf16' else F32_PEAK_TFLOPS
-        achieved = BACKBONE_FLOP * B / (bb_ms * 1e-3) / 1e12
-        n_l = max(k_n.value, 1)
-        k_avg_us = k_ms.value * 1e3 / n_l
-        k_tf = k_fl.value / (k_ms.value * 1e-3) / 1e12 if k_ms.value > 0 else 0.0
+        from sad.engine import Engine
+        # accuracy against the reference-generated fixtures (the bench model IS the golden n6 model) and
+        # against the fp32 device path over this rank's whole batch
+        fx = np.load(os.path.join(gold, 'golden_frontend.npz'))
+        gm = np.load(os.path.join(gold, 'golden_models.npz'))['n6_merged']
+        gpcm = torch.from_numpy(fx['pcm']).to(dev)
+        e32 = Engine(sd, dev, dtype='fp32', micro_batch=mbs['fp32'])
+        _, m32 = e32.forward_pcm(pcm)
+        torch.cuda.synchronize()
+        lab32 = decisions(m32)
+
+        def accuracy(mode):
+            _, mg = mode.eng.forward_pcm(gpcm)
+            torch.cuda.synchronize()
+            lab = decisions(mode.merged)
+            agree = sum(a == b for a, b in zip(lab, lab32)) / len(lab32)
+            return {'max_dlogit_golden': round(float(np.abs(mg.cpu().numpy() - gm).max()), 7),
+                    'golden_segments': int(gpcm.shape[0]),
+                    'max_dlogit_vs_fp32_device': round((mode.merged - m32).abs().max().item(), 7),
+                    'decision_agreement_vs_fp32_device': agree, 'segments_compared': B}
+
+        peak = BF16_PEAK_TFLOPS if args.dtype != 'fp32' else F32_PEAK_TFLOPS
+        fac = 3 if args.dtype == 'bf16x3' else 1
+        alg, exe, kinfo = kernel_roofline(r, fac)
         traffic = None
-        tj = os.path.join(ROOT, 'profiles', 'r01_pmc_traffic.json')
-        if os.path.exists(tj) and args.dtype == 'bf16':
-            tr = json.load(open(tj))
+        if os.path.exists(TRAFFIC_JSON) and args.dtype == 'bf16':
+            tr = json.load(open(TRAFFIC_JSON))
             rec = tr.get(DOMINANT_KERNEL) or tr.get(DOMINANT_KERNEL_OLD)
             if rec and rec.get('hbm_read_bytes') is not None:
                 traffic = rec['hbm_read_bytes'] + rec['hbm_write_bytes']
+        bb_alg = BACKBONE_FLOP * B / (r['bb_ms'] * 1e-3) / 1e12
         out = {
             'metric': '4s@32kHz segments/sec end-to-end (mel+ResNet+ensemble), 1/2/4/8 MI355X',
-            'value': round(value, 1), 'unit': 'segments/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'value': round(r['value'], 1), 'unit': 'segments/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(r['ms'], 3), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': args.dtype,
             'data': 'synthetic int16 PCM (counter-hash PRNG, generated in HBM) + random-init ResNet-18/6 heads '
-                    '(hash PRNG, BN-calibrated)',
+                    '(hash PRNG, BN-calibrated; = the golden n6 fixture model)',
             'config': {'workload': 'end-to-end inference: B int16 4 s segments resident in HBM -> mel front end '
                                    '-> ResNet-18@512x512 -> 6 binary heads -> merge (+RCCL all-gather of logits)',
-                       'segments_per_gpu_per_step': B, 'heads': args.heads, 'distinct_backbones': 1,
-                       'micro_batch': args.micro_batch, 'parallelism': f'dp{world}'},
+                       'segments_per_gpu_per_step': B, 'heads': HEADS, 'distinct_backbones': 1,
+                       'micro_batch': head.mb, 'parallelism': f'dp{world}',
+                       'per_rank_ms_per_step': r['rank_ms_per_step'], 'per_rank_allgather_ms': r['rank_gather_ms']},
             'roofline': {'bound': 'mfma',
                          'kernel': 'sad::block_conv_kernel 256x256 tile (variant 13): the layer3 + layer4 convs, '
-                                   '8 launches per micro-batch, about 35% of the step',
-                         'achieved': round(k_tf, 1), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(k_tf / peak, 4),
+                                   '8 launches per micro-batch of 512, about 35% of the bf16 step',
+                         'achieved': round(exe, 1), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(exe / peak, 4),
                          'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, '
                                                              'profiles/r01_pmc_traffic.json)',
-                         'launches': k_n.value, 'launch_avg_us': round(k_avg_us, 2),
-                         'flop_per_launch': round(k_fl.value / n_l),
-                         'backbone': {'achieved': round(achieved, 1), 'frac': round(achieved / peak, 4),
-                                      'ms_per_step': round(bb_ms, 3), 'flop_per_segment': BACKBONE_FLOP,
+                         **kinfo,
+                         'backbone': {'achieved': round(bb_alg * fac, 1), 'frac': round(bb_alg * fac / peak, 4),
+                                      'ms_per_step': round(r['bb_ms'], 3), 'flop_per_segment': BACKBONE_FLOP,
                                       'what': 'fused resize+stem + 16 block-conv GEMMs + avgpool, HIP events '
                                               'around the backbone call'},
                          'measured_gemm_ceiling_tflops': 1344.0,
                          # front end (configs[1]): fused STFT/mel/dB + standardise, fp32 VALU-bound
                          # (SURVEY 8(d): 16.4 MFLOP and 384,512 B per segment)
-                         'frontend': {'ms_per_step': round(fe_ms, 3),
-                                      'achieved_tflops': round(FE_FLOP * B / (fe_ms * 1e-3) / 1e12, 2),
+                         'frontend': {'ms_per_step': round(r['fe_ms'], 3),
+                                      'achieved_tflops': round(FE_FLOP * B / (r['fe_ms'] * 1e-3) / 1e12, 2),
                                       'peak_tflops': F32_PEAK_TFLOPS,
-                                      'frac': round(FE_FLOP * B / (fe_ms * 1e-3) / 1e12 / F32_PEAK_TFLOPS, 4),
-                                      'achieved_gbps': round(FE_BYTES * B / (fe_ms * 1e-3) / 1e9, 1),
-                                      'segments_per_s': round(B / (fe_ms * 1e-3), 1)}},
+                                      'frac': round(FE_FLOP * B / (r['fe_ms'] * 1e-3) / 1e12 / F32_PEAK_TFLOPS, 4),
+                                      'achieved_gbps': round(FE_BYTES * B / (r['fe_ms'] * 1e-3) / 1e9, 1),
+                                      'segments_per_s': round(B / (r['fe_ms'] * 1e-3), 1)}},
+            'accuracy': accuracy(head),
         }
+        if par is not None:
+            palg, pexe, pinfo = kernel_roofline(par, 3)
+            out['parity_mode'] = {
+                'dtype': 'bf16x3', 'what': 'split-bf16: hi/lo bf16 operands, 3 bf16 MFMAs per product, fp32 '
+                                           'accumulate (north-star parity mode)',
+                'value': round(par['value'], 1), 'unit': 'segments/s', 'ms_per_step': round(par['ms'], 3),
+                'steps': p_steps, 'micro_batch': par_mode.mb,
+                'per_rank_ms_per_step': par['rank_ms_per_step'],
+                'roofline': {'kernel': 'block_conv_kernel variant 13, split-bf16', 'achieved': round(pexe, 1),
+                             'unit': 'TFLOP/s (bf16 MFMA executed = 3 x algorithmic)', 'peak': BF16_PEAK_TFLOPS,
+                             'frac': round(pexe / BF16_PEAK_TFLOPS, 4), 'algorithmic_tflops': round(palg, 1),
+                             'algorithmic_frac_of_f32_peak': round(palg / F32_PEAK_TFLOPS, 4), **pinfo,
+                             'backbone_algorithmic_tflops': round(BACKBONE_FLOP * B / (par['bb_ms'] * 1e-3) / 1e12,
+                                                                  1)},
+                'accuracy': accuracy(par_mode) if par_mode is not head else out['accuracy']}
+        if world == 1 and args.fp32_steps > 0 and args.dtype != 'fp32':
+            f = Mode(sd, dev, 'fp32', mbs['fp32'], B, 1).run(pcm, args.fp32_steps, 1, profile=False)
+            out['fp32_mode'] = {'value': round(f['value'], 1), 'unit': 'segments/s', 'ms_per_step': round(f['ms'], 3),
+                                'steps': args.fp32_steps, 'peak': F32_PEAK_TFLOPS,
+                                'backbone_tflops': round(BACKBONE_FLOP * B / (f['bb_ms'] * 1e-3) / 1e12, 1)}
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline()
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -33,7 +33,7 @@ def gather_rows(local: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
     pad = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[:local.shape[0]] = local
     out = torch.empty((world * cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    if hasattr(dist, 'all_gather_into_tensor') and local.device.type == 'cuda':
+    if local.device.type == 'cuda' and dist.get_backend(group) == 'nccl':
         dist.all_gather_into_tensor(out, pad, group=group)
     else:
         dist.all_gather(list(out.chunk(world)), pad, group=group)

@@ -9,8 +9,11 @@ PRNG (sad_synth_pcm, keyed by the GLOBAL segment id, so the result does not
 depend on the world size) -- generation is timed separately and excluded from
 the inference rate, as SURVEY 8(d) prescribes.  Prints one JSON line on rank 0.
 
-    python tools/run_1m.py [--total 1000000] [--chunk 4096] [--host-fed]
-    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/run_1m.py
+    python tools/run_1m.py [--gpus N] [--total 1000000] [--chunk 4096] [--host-fed] [--dtype bf16x3]
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/run_1m.py --gpus 8
+
+``--gpus N`` without a launcher starts the N ranks itself (sad/launch.py); under
+a launcher the world size must equal N.
 
 --host-fed (SURVEY 8(d) "host-fed (pinned H2D) variant"): each chunk's int16
 PCM is copied from pinned host memory on a side stream, double-buffered and
@@ -41,18 +44,30 @@ def main(argv=None, return_logits: bool = False):
     ap.add_argument('--total', type=int, default=1_000_000)
     ap.add_argument('--chunk', type=int, default=4096, help='segments per device batch')
     ap.add_argument('--heads', type=int, default=6)
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
-    ap.add_argument('--micro-batch', type=int, default=512)
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'bf16x3', 'fp32'])
+    ap.add_argument('--micro-batch', type=int, default=0, help='0: 512 bf16, 256 bf16x3, 128 fp32')
     ap.add_argument('--host-fed', action='store_true', help='PCM from pinned host memory (H2D inside the timing)')
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'], help='gloo: tests only')
+    ap.add_argument('--one-device', action='store_true', help='every rank on cuda:0 (2-rank test on one GPU)')
+    ap.add_argument('--out-logits', default='', help='rank 0 saves the gathered logits here (tests)')
     args = ap.parse_args(argv)
+    args.micro_batch = args.micro_batch or {'bf16': 512, 'bf16x3': 256, 'fp32': 128}[args.dtype]
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+    from sad import launch
+    if args.gpus > 1 and not launch.under_launcher():
+        rc = launch.relaunch(args.gpus, os.path.abspath(__file__), sys.argv[1:] if argv is None else list(argv))
+        if argv is None:
+            sys.exit(rc)
+        return rc
+    world, rank, local = launch.check_world(args.gpus)
+    dev = torch.device('cuda', 0 if args.one_device else local)
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
 
     from sad import _lib
     from sad import weights as sw
@@ -146,6 +161,8 @@ def main(argv=None, return_logits: bool = False):
             'gathered_rows': int(allz.shape[0]), 'all_finite': finite,
             'logits_checksum': round(float(allz.double().sum().item()), 3)}
         print(json.dumps(rec), flush=True)
+        if args.out_logits:
+            torch.save(allz.cpu(), args.out_logits)
     if world > 1:
         dist.destroy_process_group()
     if return_logits:
