@@ -226,6 +226,8 @@ def main():
                                                                 '(0: max(steps // 3, 3); -1: skip)')
     ap.add_argument('--fp32-steps', type=int, default=2, help='timed steps of the fp32 mode (N = 1; 0: skip)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--kernels-only', action='store_true',
+                    help='profiling runs: only the headline mode (no parity/fp32 legs, accuracy or CPU baseline)')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'], help='gloo: tests only')
     ap.add_argument('--one-device', action='store_true', help='every rank on cuda:0 (2-rank test on one GPU)')
     args = ap.parse_args()
@@ -254,6 +256,8 @@ def main():
     head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world)
     r = head.run(pcm, args.steps, args.warmup)
     p_steps = max(args.steps // 3, 3) if args.parity_steps == 0 else args.parity_steps
+    if args.kernels_only:
+        p_steps, args.fp32_steps, args.no_cpu_baseline = -1, 0, True
     par_mode, par = None, None
     if p_steps > 0:
         if args.dtype == 'bf16x3':
@@ -269,12 +273,15 @@ def main():
         fx = np.load(os.path.join(gold, 'golden_frontend.npz'))
         gm = np.load(os.path.join(gold, 'golden_models.npz'))['n6_merged']
         gpcm = torch.from_numpy(fx['pcm']).to(dev)
-        e32 = Engine(sd, dev, dtype='fp32', micro_batch=mbs['fp32'])
-        _, m32 = e32.forward_pcm(pcm)
-        torch.cuda.synchronize()
-        lab32 = decisions(m32)
+        if not args.kernels_only:
+            e32 = Engine(sd, dev, dtype='fp32', micro_batch=mbs['fp32'])
+            _, m32 = e32.forward_pcm(pcm)
+            torch.cuda.synchronize()
+            lab32 = decisions(m32)
 
         def accuracy(mode):
+            if args.kernels_only:
+                return None
             _, mg = mode.eng.forward_pcm(gpcm)
             torch.cuda.synchronize()
             lab = decisions(mode.merged)

@@ -46,6 +46,41 @@ def _np32(t) -> np.ndarray:
     return np.ascontiguousarray(torch.as_tensor(t).detach().to('cpu', torch.float32).numpy())
 
 
+def _checked(sd: Dict[str, torch.Tensor], key: str, shape) -> np.ndarray:
+    """sd[key] as contiguous fp32, after checking its shape: the C plan builders
+    read raw host pointers with the layout's sizes, so a wrong width (e.g. a
+    wide_resnet state dict) must fail here, not overrun host memory there."""
+    if key not in sd:
+        raise KeyError(f'missing tensor {key!r}')
+    a = _np32(sd[key])
+    if tuple(a.shape) != tuple(shape):
+        raise ValueError(f'tensor {key!r} has shape {tuple(a.shape)}, expected {tuple(shape)}')
+    return a
+
+
+def _backbone_arrays(base_sd, shapes) -> list:
+    arrays = []
+    for key, shape, kind in shapes:
+        if kind == 'conv':
+            arrays.append(_checked(base_sd, f'{key}.weight', shape))
+        else:
+            for s in ('weight', 'bias', 'running_mean', 'running_var'):
+                arrays.append(_checked(base_sd, f'{key}.{s}', shape))
+    return arrays
+
+
+def _head_arrays(sd, num_features: int) -> list:
+    from .weights import head_layout
+    shapes = {}
+    for idx, kind, shape in head_layout(num_features):
+        if kind == 'linear':
+            shapes[f'{idx}.weight'], shapes[f'{idx}.bias'] = shape, shape[:1]
+        else:
+            for s in ('weight', 'bias', 'running_mean', 'running_var'):
+                shapes[f'{idx}.{s}'] = shape
+    return [_checked(sd, k, shapes[k]) for k in HEAD_KEYS]
+
+
 class FrontEnd:
     def __init__(self, device='cuda', norm: str | None = 'slaney', n_samples: int = N_SAMPLES,
                  sample_rate: int = 32000, n_fft: int = 2048, hop: int = 512, n_mels: int = 128,
@@ -133,18 +168,11 @@ class Backbone:
         self._dt = _dtype_code(dtype)
         self.tdtype = torch.float32 if dtype == 'fp32' else torch.bfloat16
         self.micro_batch = micro_batch
-        arrays = []
-        for key, _shape, kind in backbone_param_shapes():
-            if kind == 'conv':
-                arrays.append(_np32(base_sd[f'{key}.weight']))
-            else:
-                for s in ('weight', 'bias', 'running_mean', 'running_var'):
-                    arrays.append(_np32(base_sd[f'{key}.{s}']))
-        self._keep = arrays
-        ptrs = _lib.pointer_array(arrays)
+        arrays = _backbone_arrays(base_sd, backbone_param_shapes())
         self._plan = _lib.P()
         with torch.cuda.device(self.device):
-            _lib.call('sad_backbone_plan_create', ptrs, len(arrays), self._dt, MAP_H, MAP_W,
+            # the plan copies (hipMemcpy, synchronous) what it needs; the host arrays die here
+            _lib.call('sad_backbone_plan_create', _lib.pointer_array(arrays), len(arrays), self._dt, MAP_H, MAP_W,
                       _lib.ctypes.byref(self._plan))
         self._ws = None
 
@@ -220,14 +248,7 @@ class ResNetBackbone:
         # the widest activation (layer1 of a Bottleneck net: 128x128x256) must
         # stay under the kernels' 2 GiB buffer-addressing range
         self.micro_batch = max(1, min(micro_batch, 128 if dtype == 'bf16' else 64))  # fp32 / bf16x3: 4 B per value
-        arrays = []
-        for key, _shape, kind in arch_param_shapes(model_name):
-            if kind == 'conv':
-                arrays.append(_np32(base_sd[f'{key}.weight']))
-            else:
-                for s in ('weight', 'bias', 'running_mean', 'running_var'):
-                    arrays.append(_np32(base_sd[f'{key}.{s}']))
-        self._keep = arrays
+        arrays = _backbone_arrays(base_sd, arch_param_shapes(model_name))
         lay = (_lib.I32 * 4)(*layers)
         self._plan = _lib.P()
         with torch.cuda.device(self.device):
@@ -274,8 +295,7 @@ class Heads:
                  device='cuda', feat_dim: int = 512):
         self.device = _dev(device)
         self.n_heads = len(head_sds)
-        arrays = [_np32(sd[k]) for sd in head_sds for k in HEAD_KEYS]
-        self._keep = arrays
+        arrays = [a for sd in head_sds for a in _head_arrays(sd, feat_dim)]
         fi = (_lib.I32 * self.n_heads)(*feat_index)
         self._plan = _lib.P()
         with torch.cuda.device(self.device):
@@ -310,11 +330,17 @@ class Heads:
 
 
 def _arch(base_sd) -> str:
-    """Architecture name of a backbone state dict; unrecognised key sets are
-    treated as resnet18 so that the missing-key check names what is absent."""
+    """Architecture name of a backbone state dict.  A BasicBlock key set that
+    matches no depth is treated as resnet18 so that the missing-key check names
+    what is absent; a Bottleneck key set (conv3 keys) that matches no depth
+    raises -- read as resnet18 its 1x1 convs would be taken for 3x3."""
+    if not base_sd:
+        return 'resnet18'
     try:
-        return arch_of_state(base_sd) if base_sd else 'resnet18'
+        return arch_of_state(base_sd)
     except ValueError:
+        if any('.conv3.' in k for k in base_sd):
+            raise
         return 'resnet18'
 
 

@@ -7,8 +7,8 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/pmc_$TAG; rm -rf $OUT && mkdir -p $OUT
 A="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES"
 B="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
-timeout -s KILL 120 rocprofv3 --pmc $A -d $OUT/a -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@" > $OUT/a.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc $B -d $OUT/b -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@" > $OUT/b.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc $A -d $OUT/a -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --kernels-only "$@" > $OUT/a.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc $B -d $OUT/b -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --kernels-only "$@" > $OUT/b.log 2>&1
 python3 - "$OUT" > gpurun_out/pmc_$TAG.md <<'PY'
 import csv, collections, glob, sys
 out = sys.argv[1]

@@ -9,11 +9,11 @@ cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
 OUT=gpurun_out/prof_$TAG
 rm -rf $OUT && mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-  python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $OUT/trace.log 2>&1
+  python3 bench.py --steps 3 --warmup 1 --kernels-only "$@" > $OUT/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@" > $OUT/fetch.log 2>&1
+  python3 bench.py --steps 1 --warmup 1 --kernels-only "$@" > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- \
-  python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@" > $OUT/write.log 2>&1
+  python3 bench.py --steps 1 --warmup 1 --kernels-only "$@" > $OUT/write.log 2>&1
 T=$(find $OUT/trace -name 'run_kernel_trace.csv' | head -1 | xargs dirname)
 F=$(find $OUT/fetch -name 'run_counter_collection.csv' | head -1 | xargs dirname)
 W=$(find $OUT/write -name 'run_counter_collection.csv' | head -1 | xargs dirname)
