@@ -26,13 +26,35 @@
 //  * one K-step = one filter tap (or shortcut chunk) x 128 B of channels
 //    (64 bf16 / 32 f32), 8 x 16-B chunks per pixel row, XOR-swizzled through
 //    the DMA source address (LDS-DMA writes lane-linearly).
+#include <stdio.h>
+
 #include <type_traits>
+#include <vector>
 
 #include "common.hpp"
 #include "igemm.hpp"
 #include "kernels.hpp"
 
+#ifndef SAD_STAMPS
+#define SAD_STAMPS 0
+#endif
+
 namespace sad {
+
+// diagnostic build (-DSAD_STAMPS=1): s_memtime of one wave at a point of the
+// K loop (cdna_hip_programming.md 7, in-kernel stamps); never in a product build
+#define SAD_STAMP(slot)                                                                          \
+  do {                                                                                           \
+    if constexpr (SAD_STAMPS) {                                                                  \
+      if (stamp_on) {                                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        uint64_t t_;                                                                             \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        if (lane == 0) a.stamps[(size_t)stamp_wave * 4096 + (size_t)g * 4 + (slot)] = t_;        \
+      }                                                                                          \
+    }                                                                                            \
+  } while (0)
 
 // WC x WP waves; each wave owns (16*TC) channels x (16*TP) pixels (TC, TP 16x16
 // MFMA tiles); OCC = workgroups per CU the LDS budget admits.
@@ -86,6 +108,9 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   const int wc = wave / WP, wp = wave % WP;
   const int n_tc = a.Cout / BC;
   const int w = xcd_remap(blockIdx.x, gridDim.x);
+  // channel tile tc = w % n_tc: both channel tiles share an XCD's pixel tiles.
+  // (Channel tiles by contiguous w ranges -- one tile's weights per XCD L2 --
+  // measured 3-4 % slower on layer4.)
   const int tc = w % n_tc;
   const int gp = gridDim.x / n_tc, wi = w / n_tc;
   // 32-bit tile/pixel arithmetic (the launcher checks M + BP and the step count
@@ -125,7 +150,9 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   int poff0[QP], poff1[QP], piy[QP], pix[QP];
   int itile = tp_begin;
   // K cursor of the next DMA, kept incrementally (no scalar divisions per step):
-  // step iks = (ky * KW + kx) * kpt + ci of the conv taps, then the shortcut
+  // step iks = (ky * KW + kx) * kpt + ci of the conv taps, then the shortcut.
+  // (Channel-chunk-outer order -- consecutive steps re-reading one 64-channel
+  // slice shifted by a tap -- measured 2-4 % slower on layer3/4.)
   int iks = 0, ici = 0, ikx = 0, iky = 0, itoff = 0;
   const int kpt = a.Cin * ES / 128;  // K-steps per tap
   auto set_tile = [&](int tp) __attribute__((always_inline)) {
@@ -159,15 +186,24 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   const float* s_bias = LDS_BIAS ? (const float*)(smem + S * STAGE) : a.bias + c0;
   if (LDS_BIAS && tid < BC / 4) *(float4*)(smem + S * STAGE + 16 * tid) = *(const float4*)(a.bias + c0 + 4 * tid);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  auto issue = [&](int st) __attribute__((always_inline)) {
+  // one DMA piece k of K-step `iks` into stage st: k < QP pixel rows, else weight rows
+  auto issue_piece = [&](int st, int k) __attribute__((always_inline)) {
     const unsigned sb = lds0 + st * STAGE;
-    if (iks < nk0) {
-#pragma unroll
-      for (int i = 0; i < QP; ++i) {
-        const int iy = piy[i] + iky, ix = pix[i] + ikx;
+    if (k < QP) {
+      if (iks < nk0) {
+        const int iy = piy[k] + iky, ix = pix[k] + ikx;
         const bool ok = ((unsigned)iy < (unsigned)a.H) && ((unsigned)ix < (unsigned)a.W);
-        dma16_m0(r0, ok ? poff0[i] + itoff : 0x7FFFFFF0, sb + (wave + NW * i) * 1024);
+        dma16_m0(r0, ok ? poff0[k] + itoff : 0x7FFFFFF0, sb + (wave + NW * k) * 1024);
+      } else {
+        dma16_m0(r1, poff1[k] + (iks - nk0) * 128, sb + (wave + NW * k) * 1024);
       }
+    } else {
+      dma16_m0(rw, woff[k - QP] + iks * 128, sb + BP * 128 + (wave + NW * (k - QP)) * 1024);
+    }
+  };
+  // advance the K cursor past step iks (and to the next tile)
+  auto issue_advance = [&]() __attribute__((always_inline)) {
+    if (iks < nk0) {
       itoff += 128;
       if (++ici == kpt) {
         ici = 0;
@@ -178,17 +214,16 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
           ++iky;
         }
       }
-    } else {
-      const int toff = (iks - nk0) * 128;
-#pragma unroll
-      for (int i = 0; i < QP; ++i) dma16_m0(r1, poff1[i] + toff, sb + (wave + NW * i) * 1024);
     }
-#pragma unroll
-    for (int i = 0; i < QW; ++i) dma16_m0(rw, woff[i] + iks * 128, sb + BP * 128 + (wave + NW * i) * 1024);
     if (++iks == nk) {
       iks = ici = ikx = iky = itoff = 0;
       if (++itile < tp_end) set_tile(itile);
     }
+  };
+  auto issue = [&](int st) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < QP + QW; ++k) issue_piece(st, k);
+    issue_advance();
   };
 
   f32x4 acc[TC][TP];
@@ -203,7 +238,12 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   int st = 0, cks = 0;
   int ctile = tp_begin;
   T* __restrict__ out = (T*)a.out;
+  // stamps: workgroup 0, waves 0 and NW/2 (the two waves of SIMD 0's pair), steps < 1024
+  const bool stamp_on0 = SAD_STAMPS && a.stamps && blockIdx.x == 0 && (wave == 0 || wave == NW / 2);
+  const int stamp_wave = wave == 0 ? 0 : 1;
   for (int g = 0; g < total; ++g) {
+    const bool stamp_on = stamp_on0 && g < 1024;
+    SAD_STAMP(0);
     // retire this wave's DMA for step g (S = 3: step g+1's stays in flight;
     // epilogue stores issued since are waited for conservatively), then the
     // barrier publishes every wave's step-g data and frees the stage the next
@@ -216,6 +256,7 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
     }
     if (!(a.ablate & 4)) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    SAD_STAMP(1);
     const bool do_issue = g + S - 1 < total && !(a.ablate & 1);
     const int ist = S == 3 ? (st == 0 ? 2 : st - 1) : (st ^ 1);
     const char* base = smem + st * STAGE;
@@ -237,15 +278,27 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
         const int r = wp * 16 * TP + j * 16 + fr;
         pf[j] = *(const uint4*)(base + r * 128 + (swz(r, fg) << 4));
       }
-      if (do_issue) issue(ist);
+      // SIMD partners split in time: waves 0..NW/2-1 issue the ring's DMA
+      // pieces before their MFMAs, waves NW/2.. after weight row SR of half 0,
+      // so one wave's DMA issue (~100 cycles a piece, in-kernel stamps) overlaps
+      // its partner's MFMAs instead of both idling the SIMD's matrix pipe.
+      // Same-box A/B (bench, 3 rounds): bf16 SR = 8: layer3/4 launches -3.5 %,
+      // +0.6 % end to end (SR = 4: +0.4 %, 2: -0.1 %); split-bf16 SR = 2: +1 %
+      // (SR = 8 spills: 1443 vs 600 us)
+      const bool dma_late = wave >= NW / 2;
+      if (do_issue && !dma_late) issue(ist);
       __builtin_amdgcn_sched_barrier(0);
+      SAD_STAMP(2);
 #pragma unroll
       for (int j = 0; j < TP; ++j) {
         const int r = wp * 16 * TP + j * 16 + fr;
         pg[j] = *(const uint4*)(base + r * 128 + (swz(r, fg + 4) << 4));
       }
-#pragma unroll
-      for (int i = 0; i < TC; ++i) {
+      // half 0: per weight row i its TP (X3: 2 TP) MFMAs, then the read of its
+      // half-1 fragment into the freed registers; the late waves' DMA goes in
+      // after row SR
+      constexpr int SR = X3 ? 2 : TC;
+      auto half0_row = [&](int i) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pf[j], acc[i][j]);
         if constexpr (X3) {  // W_hi . X_lo while W_hi is still in registers
@@ -254,20 +307,34 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
         }
         const int r = BP + wc * 16 * TC + i * 16 + fr;
         wf[i] = *(const uint4*)(base + r * 128 + (swz(r, fg + 4) << 4));
-      }
-      // order: half 1's pixel reads, then per weight row i its TP (X3: 2 TP)
-      // MFMAs followed by the read of its half-1 fragment
+      };
+#pragma unroll
+      for (int i = 0; i < SR; ++i) half0_row(i);
+      // order: half 1's pixel reads, then per row its MFMAs and its read
       __builtin_amdgcn_sched_group_barrier(0x100, TP, 0);
 #pragma unroll
-      for (int i = 0; i < TC; ++i) {
+      for (int i = 0; i < SR; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, X3 ? 2 * TP : TP, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if (do_issue && dma_late) issue(ist);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (SR < TC) {
+#pragma unroll
+        for (int i = SR; i < TC; ++i) half0_row(i);
+#pragma unroll
+        for (int i = SR; i < TC; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, X3 ? 2 * TP : TP, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int i = 0; i < TC; ++i)
 #pragma unroll
         for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], X3 ? pf[j] : pg[j], acc[i][j]);  // X3: W_lo . X_hi
+      SAD_STAMP(3);
     } else {
     if (do_issue) issue(ist);
     // both K-halves' fragments in registers; half 1's reads are issued between
@@ -364,7 +431,7 @@ if constexpr (X3) {
 #pragma unroll
       for (int j = 0; j < TP; ++j) {
         const int px = ctile * BP + wp * 16 * TP + j * 16 + fr;
-        if (out != nullptr && px < M) {
+        if (out != nullptr && px < M && !(a.ablate & 8)) {
           // epilogue residual (a Bottleneck's identity shortcut): the pixel's TC
           // 4-channel groups are loaded together, before any of its stores (the
           // compiler cannot move a load above a store that may alias it, so
@@ -521,7 +588,7 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
   return SAD_ERR_ARG;
 }
 
-int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s);
+int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s, bool x3 = false);
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s);
 
 // halo kernel (variant 20): bf16 stride-1 3x3 with Cout <= 128 (layer1, layer2's
@@ -529,9 +596,11 @@ int launch_halo_rw(const BlockConvArgs& a, hipStream_t s);
 // mb 128: layer1 c2 261 vs 350 us, layer2 c1 187 vs 218 us); for Cout >= 256
 // the patch would be re-loaded per 64-channel tile.  It is also the only
 // kernel taking `res`.
+// (split-bf16: logical channels; the kernel sees 2 Cin bf16 channels)
 static bool halo_ok(const BlockConvArgs& a, int dtype) {
-  return dtype == SAD_BF16 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.in1 && a.Cin % 64 == 0 &&
-         a.Cout % 64 == 0 && a.W % 16 == 0 && a.H % 16 == 0;
+  return (dtype == SAD_BF16 || dtype == SAD_BF16X3) && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 &&
+         !a.in1 && a.Cin % (dtype == SAD_BF16X3 ? 32 : 64) == 0 && a.Cout % 64 == 0 && a.W % 16 == 0 &&
+         a.H % 16 == 0;
 }
 // SAD_L2_HALO=0 runs layer2's second block on the implicit-GEMM kernel (identity
 // shortcut as MFMA columns) instead of the halo kernel (A/B switch)
@@ -554,6 +623,9 @@ static int c128_variant() {
   return v;
 }
 int default_block_variant(const BlockConvArgs& a, int dtype) {
+  // split-bf16: the halo kernel for the stride-1 convs of layer1 (Cout 64) and
+  // layer2 (Cout 128), whose implicit GEMM is L2->LDS-fill bound
+  if (dtype == SAD_BF16X3) return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
   if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo()))) return 20;
   return a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9);
@@ -576,6 +648,35 @@ static bool variant_fits(int v, int cout) {
   if (v == 25) return cout == 64;
   return v >= 9 && v <= 18 && cout % bc[v] == 0;
 }
+
+#if SAD_STAMPS
+// diagnostic build: stamp the launch, synchronise, print the per-step phase
+// averages (cycles) of wave 0 and wave NW/2 of workgroup 0 to stderr
+static int stamp_report(const BlockConvArgs& a, hipStream_t s) {
+  std::vector<uint64_t> h(2 * 4096);
+  SAD_CHECK_HIP(hipStreamSynchronize(s));
+  SAD_CHECK_HIP(hipMemcpy(h.data(), a.stamps, h.size() * 8, hipMemcpyDeviceToHost));
+  for (int w = 0; w < 2; ++w) {
+    double ph[4] = {0, 0, 0, 0};
+    int n = 0;
+    for (int g = 8; g + 1 < 1024; ++g) {
+      const uint64_t* t = &h[w * 4096 + g * 4];
+      const uint64_t t0n = h[w * 4096 + (g + 1) * 4];
+      if (!t[0] || !t[3] || !t0n || t0n < t[3]) break;
+      ph[0] += (double)(t[1] - t[0]);
+      ph[1] += (double)(t[2] - t[1]);
+      ph[2] += (double)(t[3] - t[2]);
+      ph[3] += (double)(t0n - t[3]);
+      ++n;
+    }
+    if (n)
+      fprintf(stderr, "stamps M=%lld Cout=%d K=%d wave %d: %d steps, cycles/step wait+barrier %.0f | reads+dma %.0f | "
+              "mfma issue %.0f | tail %.0f | total %.0f\n", (long long)a.M, a.Cout, a.KH * a.KW * a.Cin, w, n,
+              ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, (ph[0] + ph[1] + ph[2] + ph[3]) / n);
+  }
+  return SAD_OK;
+}
+#endif
 
 int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int variant) {
   SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16 || dtype == SAD_BF16X3, "dtype");
@@ -607,8 +708,12 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   SAD_REQUIRE(a.Cout % 64 == 0 && a.out_pstride % 4 == 0, "Cout / output stride");
   SAD_REQUIRE(a.in0_pstride % (16 / ES) == 0 && (!a.in1 || a.in1_pstride % (16 / ES) == 0), "input strides");
   if (a.M == 0) return SAD_OK;
-  const int v = variant > 0 ? variant : default_block_variant(a, dtype);
+  const int v = variant > 0 ? variant : default_block_variant(a_in, dtype);
   SAD_REQUIRE(variant_fits(v, a.Cout), "variant's channel tile does not divide Cout");
+  if (dtype == SAD_BF16X3 && (v == 20 || v == 21)) {
+    SAD_REQUIRE(v == 20 && halo_ok(a_in, dtype), "split-bf16 halo conv: variant 20, 3x3/s1/p1, H, W % 16");
+    return launch_halo_v(a, v, s, true);
+  }
   if (v == 25) {
     SAD_REQUIRE(halo_ok(a, dtype), "halo conv (variant 25): bf16, 3x3/s1/p1, no GEMM shortcut, H, W % 16");
     return launch_halo_rw(a, s);
@@ -618,11 +723,23 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
     return launch_halo_v(a, v, s);
   }
   SAD_REQUIRE(!a.res || a.res_pstride % 4 == 0, "residual pixel stride must keep 4-channel alignment");
+#if SAD_STAMPS
+  static uint64_t* stamp_buf = nullptr;
+  if (!stamp_buf) SAD_CHECK_HIP(hipMalloc(&stamp_buf, 2 * 4096 * 8));
+  SAD_CHECK_HIP(hipMemsetAsync(stamp_buf, 0, 2 * 4096 * 8, s));
+  a.stamps = stamp_buf;
+#endif
+  int rc;
   if (dtype == SAD_BF16X3) {
     SAD_REQUIRE(v >= 9 && v <= 18, "split-bf16 runs on the implicit-GEMM variants 9..18");
-    return launch_block_v<u16, true>(a, v, s);
+    rc = launch_block_v<u16, true>(a, v, s);
+  } else {
+    rc = dtype == SAD_BF16 ? launch_block_v<u16>(a, v, s) : launch_block_v<float>(a, v, s);
   }
-  return dtype == SAD_BF16 ? launch_block_v<u16>(a, v, s) : launch_block_v<float>(a, v, s);
+#if SAD_STAMPS
+  if (rc == SAD_OK && v == 13) rc = stamp_report(a, s);
+#endif
+  return rc;
 }
 
 }  // namespace sad

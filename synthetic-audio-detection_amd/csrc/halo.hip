@@ -57,7 +57,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 // groups of MI355X_MICROARCH.md "LDS").
 __device__ __forceinline__ int hswz(int row, int chunk) { return chunk ^ (row & 6); }
 
-template <int WC, int WP, int TC, int TP, int TW>
+template <int WC, int WP, int TC, int TP, int TW, bool X3 = false>
 struct HaloGeo {
   static constexpr int NW = WC * WP;
   static constexpr int NL = NW / 2;             // waves per role
@@ -79,7 +79,10 @@ struct HaloGeo {
   // step), the tile's residual rows over taps [2, 2 + RT)
   static constexpr int PT = QP <= 12 ? 4 : 7;
   static constexpr int RT = 4;
-  static constexpr int OFF_RES = 2 * PATCH, OFF_W = 2 * PATCH + RES;
+  // X3 (split-bf16): no LDS staging -- the residual comes into registers and
+  // the epilogue stores hi/lo straight from them (the staging rows would be
+  // 256 B per pixel and not fit beside the ring)
+  static constexpr int OFF_RES = 2 * PATCH, OFF_W = 2 * PATCH + (X3 ? 0 : RES);
   static constexpr int SMEM = OFF_W + NWS * WST;
   static_assert(TW == 16, "a 16-pixel fragment is one tile row");
   static_assert(BP % TW == 0 && NW % 2 == 0, "tile shape");
@@ -87,9 +90,13 @@ struct HaloGeo {
   static_assert(QP <= 3 * PT && PT <= 8, "patch pieces must be issued before the next chunk's last tap");
 };
 
-template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU>
+// X3: split-bf16 parity mode (block.hip): channels [hi 32 | lo 32] per 64-bf16
+// chunk, so a K-step's halves are hi and lo; three MFMA sets per step; the
+// epilogue adds the residual (hi + lo, loaded into registers during the
+// tile's last chunk) and stores hi/lo from registers.
+template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU, bool X3 = false>
 __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(BlockConvArgs a) {
-  using G = HaloGeo<WC, WP, TC, TP, TW>;
+  using G = HaloGeo<WC, WP, TC, TP, TW, X3>;
   constexpr int NL = G::NL, BC = G::BC, TH = G::TH, PW = G::PW, PR = G::PR;
   constexpr int QP = G::QP, QR = G::QR, QW = G::QW, NDP = G::NDP, NWS = G::NWS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -161,7 +168,7 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
     prep_patch();
   };
   auto res_pieces = [&](int t, int tap) __attribute__((always_inline)) {
-    if constexpr (RES) {
+    if constexpr (RES && !X3) {
       const __amdgpu_buffer_rsrc_t rr =
           __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.res_bytes, 0x00020000);
       const int b = t / tiles_img, rem = t - b * tiles_img;
@@ -199,6 +206,60 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
   // epilogue, part 1 (every wave, tap 0 of the next tile): bias [+ residual],
   // activation, bf16 -> the tile's LDS staging rows (in place over the
   // residual rows: each lane writes exactly the bytes it read)
+  // X3: residual (hi, lo) of the tile in registers, loaded during its last chunk
+  uint2 xres[X3 && RES ? TP : 1][X3 && RES ? TC : 1][2];
+  auto x3_pix = [&](int t, int j) __attribute__((always_inline)) {
+    const int b = t / tiles_img, rem = t - b * tiles_img;
+    const int oy = (rem / tiles_x) * TH + wp * TP + j, ox = (rem % tiles_x) * TW + (lane & 15);
+    return (int64_t)(b * a.Ho + oy) * a.Wo + ox;
+  };
+  auto x3_load_res = [&](int t, int j) __attribute__((always_inline)) {
+    if constexpr (X3 && RES) {
+      const u16* rp = (const u16*)a.res + x3_pix(t, j) * a.res_pstride;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const int co = c0 + wc * 16 * TC + i * 16 + (lane >> 4) * 4;
+        const int pc = ((co >> 5) << 6) + (co & 31);
+        xres[j][i][0] = *(const uint2*)(rp + pc);
+        xres[j][i][1] = *(const uint2*)(rp + pc + 32);
+      }
+    }
+  };
+  auto x3_epilogue = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      u16* op = (u16*)a.out + x3_pix(t, j) * a.out_pstride;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const int co = c0 + wc * 16 * TC + i * 16 + (lane >> 4) * 4;
+        const int pc = ((co >> 5) << 6) + (co & 31);
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[i][r];
+        if constexpr (RES) {
+          const uint2 h = xres[j][i][0], l = xres[j][i][1];
+          v[0] += __uint_as_float(h.x << 16) + __uint_as_float(l.x << 16);
+          v[1] += __uint_as_float(h.x & 0xFFFF0000u) + __uint_as_float(l.x & 0xFFFF0000u);
+          v[2] += __uint_as_float(h.y << 16) + __uint_as_float(l.y << 16);
+          v[3] += __uint_as_float(h.y & 0xFFFF0000u) + __uint_as_float(l.y & 0xFFFF0000u);
+        }
+        if constexpr (RELU)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        u16 hh[4], ll[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          hh[r] = f2bf(v[r]);
+          ll[r] = f2bf(v[r] - bf2f(hh[r]));
+        }
+        *(uint2*)(op + pc) =
+            make_uint2((uint32_t)hh[0] | ((uint32_t)hh[1] << 16), (uint32_t)hh[2] | ((uint32_t)hh[3] << 16));
+        *(uint2*)(op + pc + 32) =
+            make_uint2((uint32_t)ll[0] | ((uint32_t)ll[1] << 16), (uint32_t)ll[2] | ((uint32_t)ll[3] << 16));
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
   auto epilogue = [&]() __attribute__((always_inline)) {
     // every residual read issued before the first in-place write (the compiler
     // cannot prove the lanes' read and write addresses disjoint across (i, j))
@@ -277,12 +338,26 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
         p[s][j] = *(const uint4*)(pb + r * 128 + (hswz(r, c) << 4));
       }
     }
+    if constexpr (X3) {  // W_hi.X_hi (half 0 only), then W_lo.X_hi and W_hi.X_lo
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) mfma_chunk<u16>(w[0][i], p[0][j], acc[i][j]);
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) {
+          mfma_chunk<u16>(w[1][i], p[0][j], acc[i][j]);
+          mfma_chunk<u16>(w[0][i], p[1][j], acc[i][j]);
+        }
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < TC; ++i)
 #pragma unroll
         for (int j = 0; j < TP; ++j) mfma_chunk<u16>(w[s][i], p[s][j], acc[i][j]);
+    }
     // schedule: half 0's reads, then its MFMAs interleaved with half 1's reads
     __builtin_amdgcn_sched_group_barrier(0x100, TC + TP, 0);
 #pragma unroll
@@ -290,7 +365,7 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * TC * TP - (TC + TP), 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, (X3 ? 3 : 2) * TC * TP - (TC + TP), 0);
   };
 
   // ---- prologue: patch of the first chunk, weights of the first NWS-1 steps,
@@ -327,7 +402,7 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next chunk's patch + this tile's residual
         }
       }
-      if constexpr (tap == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging rows written
+      if constexpr (tap == 1 && !X3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging rows written
       if (!(ab & 4)) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (!(ab & 1)) {
@@ -341,14 +416,21 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
                 dma16_m0(r0, poff[k], lds0 + (pbuf ^ 1) * G::PATCH + (lw + NL * k) * 1024);
             if constexpr (tap == G::PT - 1) advance_patch();
           }
-          if constexpr (tap == 1)
+          if constexpr (tap == 1 && !X3)
             if (after_tile) store_tile(t - 1);
           if constexpr (RES && tap >= 2 && tap < 2 + G::RT)
             if (last_chunk) res_pieces(t, tap);
         }
       }
+      if constexpr (X3 && RES && tap >= 2 && tap < 2 + TP)
+        if (last_chunk) x3_load_res(t, tap - 2);
       if constexpr (tap == 0)
-        if (after_tile && !(ab & 8)) epilogue();
+        if (after_tile && !(ab & 8)) {
+          if constexpr (X3)
+            x3_epilogue(t - 1);
+          else
+            epilogue();
+        }
       compute_step(tap, wsc, pbuf);
       wsc = wsc + 1 == NWS ? 0 : wsc + 1;
     });
@@ -362,6 +444,10 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
   for (int c = 0; c < nchunks; ++c) chunk();
   // last tile: its residual rows were issued in its last chunk; publish, then store
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (X3) {
+    x3_epilogue(tp_end - 1);
+    return;
+  }
   __builtin_amdgcn_s_barrier();
   epilogue();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -607,13 +693,13 @@ int launch_halo_rw(const BlockConvArgs& a, hipStream_t s) {
   return a.relu ? launch_halo_rw_t<false, true>(a, s) : launch_halo_rw_t<false, false>(a, s);
 }
 
-template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU>
+template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU, bool X3>
 static int launch_halo_t(const BlockConvArgs& a, hipStream_t s) {
-  using G = HaloGeo<WC, WP, TC, TP, TW>;
+  using G = HaloGeo<WC, WP, TC, TP, TW, X3>;
   static_assert(G::SMEM <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)halo_conv_kernel<WC, WP, TC, TP, TW, RES, RELU>,
+    (void)hipFuncSetAttribute((const void*)halo_conv_kernel<WC, WP, TC, TP, TW, RES, RELU, X3>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
     attr = true;
   }
@@ -629,24 +715,29 @@ static int launch_halo_t(const BlockConvArgs& a, hipStream_t s) {
   SAD_REQUIRE(tiles_p * 9 * (a.Cin / 64) < (1ll << 31), "too many tiles for one launch");
   int64_t g = std::min<int64_t>(tiles_p * n_tc, 256);
   g = std::max<int64_t>(n_tc, g / n_tc * n_tc);
-  hipLaunchKernelGGL((halo_conv_kernel<WC, WP, TC, TP, TW, RES, RELU>), dim3((unsigned)g), dim3(64 * WC * WP),
+  if (X3) SAD_REQUIRE(a.out_pstride % 64 == 0 && (!a.res || a.res_pstride % 64 == 0), "split-bf16 pixel strides");
+  hipLaunchKernelGGL((halo_conv_kernel<WC, WP, TC, TP, TW, RES, RELU, X3>), dim3((unsigned)g), dim3(64 * WC * WP),
                      G::SMEM, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }
 
-template <int WC, int WP, int TC, int TP, int TW>
+template <int WC, int WP, int TC, int TP, int TW, bool X3 = false>
 static int launch_halo_g(const BlockConvArgs& a, hipStream_t s) {
-  if (a.res) return a.relu ? launch_halo_t<WC, WP, TC, TP, TW, true, true>(a, s)
-                           : launch_halo_t<WC, WP, TC, TP, TW, true, false>(a, s);
-  return a.relu ? launch_halo_t<WC, WP, TC, TP, TW, false, true>(a, s)
-                : launch_halo_t<WC, WP, TC, TP, TW, false, false>(a, s);
+  if (a.res) return a.relu ? launch_halo_t<WC, WP, TC, TP, TW, true, true, X3>(a, s)
+                           : launch_halo_t<WC, WP, TC, TP, TW, true, false, X3>(a, s);
+  return a.relu ? launch_halo_t<WC, WP, TC, TP, TW, false, true, X3>(a, s)
+                : launch_halo_t<WC, WP, TC, TP, TW, false, false, X3>(a, s);
 }
 
 // Variants (channels x tile (TH x TW), waves, wave tile, LDS; one WG per CU):
 //  20: 64 x 16x16  8w  64x32  154 KB
 //  21: 64 x 16x16  4w  64x64  156 KB (one wave per SIMD: half the LDS fragment reads per MFMA)
-int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s) {
+int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s, bool x3) {
+  if (x3) {
+    SAD_REQUIRE(v == 20, "split-bf16 halo conv: variant 20");
+    return launch_halo_g<1, 8, 4, 2, 16, true>(a, s);
+  }
   switch (v) {
     case 20: return launch_halo_g<1, 8, 4, 2, 16>(a, s);
     case 21: return launch_halo_g<1, 4, 4, 4, 16>(a, s);

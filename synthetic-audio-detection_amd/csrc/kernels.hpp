@@ -51,6 +51,7 @@ struct BlockConvArgs {
                          // 8 no epilogue, 16 no weight DMA, 32 no patch DMA (halo)
   float* pool_out;       // optional fused global average pool, fp32 [N, Cout] (the variant's pixel tile
                          // must be one image: block_conv_can_pool); out may then be null
+  uint64_t* stamps;      // diagnostic builds only (-DSAD_STAMPS): s_memtime stamps per K-step
 };
 
 struct StemArgs {

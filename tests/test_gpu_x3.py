@@ -79,6 +79,28 @@ def test_block_conv_x3_vs_float64(cin, cout, H, stride, shortcut, variant):
     assert err <= 1e-4, err
 
 
+@pytest.mark.parametrize('c,H,res', [(64, 32, True), (64, 48, False), (128, 16, True), (128, 32, False)])
+def test_halo_conv_x3_vs_float64(c, H, res):
+    """The split-bf16 halo kernel (variant 20: layer1 / layer2 stride-1 convs,
+    identity shortcut as an epilogue residual) vs float64."""
+    from sad.engine import block_conv, from_split, to_split
+    g = torch.Generator().manual_seed(c + H + int(res))
+    N = 3
+    x = torch.randn(N, H, H, c, generator=g).clamp_min(0)
+    r = torch.randn(N, H, H, c, generator=g).clamp_min(0) if res else None
+    w = torch.randn(c, c, 3, 3, generator=g) * (2.0 / (9 * c)) ** 0.5
+    bias = torch.randn(c, generator=g) * 0.1
+    y = F.conv2d(x.permute(0, 3, 1, 2).double(), w.double(), bias.double(), padding=1).permute(0, 2, 3, 1)
+    ref = (y + (r.double() if res else 0)).clamp_min(0)
+    wk = w.permute(0, 2, 3, 1).reshape(c, 9 * c)
+    out = block_conv(to_split(x).to(DEV), to_split(wk).to(DEV), bias.to(DEV), variant=20, split=True,
+                     res=to_split(r).to(DEV) if res else None)
+    torch.cuda.synchronize()
+    err = ((from_split(out.cpu()).double() - ref).abs().max() / ref.abs().max()).item()
+    print(f'x3 halo conv c{c} H{H} res={res}: rel err {err:.3e}')
+    assert err <= 1e-4, err
+
+
 def test_stem_x3_vs_oracle(golden_frontend):
     from oracle import frontend as ofe
     from oracle import resnet as ores

@@ -6,7 +6,7 @@ for i in $(seq $N); do
   for cfg in $1; do
     lib=${cfg%%:*}; envs=${cfg#*:}; [ "$envs" = "$cfg" ] && envs=""
     L=synthetic-audio-detection_amd/sad/libsad.so; [ "$lib" != tree ] && L=abl/libsad_$lib.so
-    r=$(env SAD_LIB=$L ${envs//,/ } timeout -k 10 120 python bench.py --no-cpu-baseline --steps 10 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], r["launch_avg_us"], r["backbone"]["ms_per_step"], r.get("frontend", {}).get("ms_per_step"))') || exit 1
+    r=$(env SAD_LIB=$L ${envs//,/ } timeout -k 10 120 python bench.py --kernels-only --steps 20 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], r["launch_avg_us"], r["backbone"]["ms_per_step"], r.get("frontend", {}).get("ms_per_step"))') || exit 1
     echo "$cfg: $r"
   done
 done

@@ -40,10 +40,12 @@ def main():
     ap.add_argument('--shapes', nargs='*', default=None)
     ap.add_argument('--blocks', action='store_true', help='sweep the block-conv kernels (variants 9-18, 20)')
     ap.add_argument('--ablate', type=int, nargs='+', default=[0], help='block kernel timing ablations (bit mask)')
+    ap.add_argument('--split', action='store_true', help='split-bf16 (bf16x3) operands; FLOP/s count 3 MFMA '
+                                                         'products per MAC in the "exec" column')
     args = ap.parse_args()
     if args.blocks:
         bench_blocks(args.mb, [v for v in args.variants if v >= 9] or list(range(9, 19)) + [20], args.iters, args.shapes,
-                     tuple(args.ablate))
+                     tuple(args.ablate), args.split)
         return
     dev = torch.device('cuda:0')
     torch.manual_seed(0)
@@ -102,9 +104,10 @@ BLOCKS = [  # name, H(in), Cin, Cout, stride, shortcut
 ]
 
 
-def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,)):
-    from sad.engine import block_conv
+def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,), split=False):
+    from sad.engine import block_conv, to_split
     dev = torch.device('cuda:0')
+    cvt = (lambda t: to_split(t.float())) if split else (lambda t: t)
     for name, H, Cin, Cout, s, sc in BLOCKS:
         if shapes and name not in shapes:
             continue
@@ -113,15 +116,15 @@ def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,)):
         h0 = H if sc is None else Ho
         cin1 = Cout // 2  # the downsample reads the previous stage's map (Cout/2 channels, 2x the side)
         K = 9 * cin0 + (0 if sc is None else (Cout if sc == 'id' else cin1))
-        w = (torch.randn(Cout, K, device=dev) * (1.0 / K) ** 0.5).to(torch.bfloat16)
+        w = cvt((torch.randn(Cout, K, device=dev) * (1.0 / K) ** 0.5).to(torch.bfloat16))
         bias = torch.randn(Cout, device=dev) * 0.1
         for mb in mbs:
-            x = torch.randn(mb, h0, h0, cin0, device=dev).to(torch.bfloat16)
+            x = cvt(torch.randn(mb, h0, h0, cin0, device=dev).to(torch.bfloat16))
             scx = None
             if sc == 'id':
-                scx = torch.randn(mb, Ho, Ho, Cout, device=dev).to(torch.bfloat16)
+                scx = cvt(torch.randn(mb, Ho, Ho, Cout, device=dev).to(torch.bfloat16))
             elif sc == 'ds':
-                scx = torch.randn(mb, 2 * Ho, 2 * Ho, cin1, device=dev).to(torch.bfloat16)
+                scx = cvt(torch.randn(mb, 2 * Ho, 2 * Ho, cin1, device=dev).to(torch.bfloat16))
             stride = s if sc is None else 1
             flop = 2.0 * mb * Ho * Ho * Cout * K
             ref = None
@@ -134,7 +137,7 @@ def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,)):
                 kw = dict(res=scx) if v in (20, 21, 25) else dict(sc=scx, sc_stride=2 if sc == 'ds' else 1)
 
                 def run(o=None):
-                    return block_conv(x, w, bias, stride, 1, relu=True, variant=v0, out=o, **kw)
+                    return block_conv(x, w, bias, stride, 1, relu=True, variant=v0, out=o, split=split, **kw)
                 out = run()
                 torch.cuda.synchronize()
                 same = 'ref' if ref is None else ('same' if torch.equal(out, ref) else
@@ -150,8 +153,9 @@ def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,)):
                     ts.append(e0.elapsed_time(e1))
                 ts.sort()
                 t = ts[len(ts) // 2]
-                print(f'{name:9s} mb={mb:4d} v={v} ablate={v0 >> 8}: {t * 1e3:9.1f} us  {flop / t / 1e9:7.1f} TF/s  {same}',
-                      flush=True)
+                ex = f'  exec {3 * flop / t / 1e9:7.1f} TF/s' if split else ''
+                print(f'{name:9s} mb={mb:4d} v={v} ablate={v0 >> 8}: {t * 1e3:9.1f} us  {flop / t / 1e9:7.1f} TF/s{ex}  '
+                      f'{same}', flush=True)
 
 
 if __name__ == '__main__':
