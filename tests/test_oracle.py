@@ -165,3 +165,49 @@ def test_synth_deterministic():
     assert np.array_equal(a, b) and a.dtype == np.int16 and a.shape == (128000,)
     assert not np.array_equal(a, synth_segment(0, 6))
     assert 2500 < a.astype(np.float64).std() < 12000 and np.abs(a).max() > 32
+
+
+def test_oracle_bottleneck_resnet50_vs_transformers():
+    """The Bottleneck restatement (resnet50: timm v1.5 layout, stride on the 3x3,
+    1x1/s + BN downsample) equals transformers.ResNetModel(layer_type='bottleneck',
+    downsample_in_bottleneck=False) given the same weights and BN statistics --
+    an independent implementation pinning the oracle the deep-backbone GPU
+    tests compare against (timm itself is not installed)."""
+    from transformers import ResNetConfig, ResNetModel
+    from oracle import resnet as ores
+    torch.manual_seed(1)
+    ours = ores.create_model('resnet50').eval()
+    for mod in ours.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_mean.uniform_(-0.1, 0.1)
+            mod.running_var.uniform_(0.5, 1.5)
+            mod.weight.data.uniform_(0.3, 0.8)
+            mod.bias.data.uniform_(-0.1, 0.1)
+    cfg = ResNetConfig(num_channels=3, embedding_size=64, hidden_sizes=[256, 512, 1024, 2048], depths=[3, 4, 6, 3],
+                       layer_type='bottleneck', hidden_act='relu', downsample_in_first_stage=False,
+                       downsample_in_bottleneck=False)
+    hf = ResNetModel(cfg).eval()
+    src = ours.state_dict()
+
+    def bn(dst, s):
+        return {f'{dst}.{k}': src[f'{s}.{k}'] for k in ('weight', 'bias', 'running_mean', 'running_var')}
+    m = {'embedder.embedder.convolution.weight': src['conv1.weight']}
+    m.update(bn('embedder.embedder.normalization', 'bn1'))
+    for li, n in enumerate((3, 4, 6, 3)):
+        for b in range(n):
+            d, s = f'encoder.stages.{li}.layers.{b}', f'layer{li + 1}.{b}'
+            for j in range(3):
+                m[f'{d}.layer.{j}.convolution.weight'] = src[f'{s}.conv{j + 1}.weight']
+                m.update(bn(f'{d}.layer.{j}.normalization', f'{s}.bn{j + 1}'))
+            if f'{s}.downsample.0.weight' in src:
+                m[f'{d}.shortcut.convolution.weight'] = src[f'{s}.downsample.0.weight']
+                m.update(bn(f'{d}.shortcut.normalization', f'{s}.downsample.1'))
+    missing, unexpected = hf.load_state_dict(m, strict=False)
+    assert not [k for k in missing if 'num_batches_tracked' not in k], missing
+    assert not unexpected, unexpected
+    x = torch.randn(2, 3, 64, 64)
+    with torch.no_grad():
+        a = ours.forward_features(x)
+        b = hf(x).last_hidden_state
+    assert a.shape == b.shape == (2, 2048, 2, 2)
+    assert ((a - b).abs().max() / b.abs().max()).item() <= 1e-5
