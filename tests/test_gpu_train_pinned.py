@@ -1,0 +1,127 @@
+"""GPU: the drop-in trainer (submodel_trainer.train / validate on the device
+Trainer) against the fixture the REFERENCE's own train() and validate() wrote
+(tests/golden/make_golden_train.py, submodel_trainer.py:241-385 under stubs):
+two epochs of two 4-segment steps, layer3 unfrozen at epoch 1 after the
+optimizer was built (quirk C4), then validation.
+
+Inputs: the same synthetic waves (sad.synth seed 13); the reference ran on the
+oracle front end's val images, the device on its own front end with the
+augmentation switched off (no mask, crop = whole image), which agree to 5e-4.
+Tolerances (fp32): loss / epoch loss relative 1e-3; pre-clip total norm 2e-3;
+clipped per-tensor gradient norms (layer3 and layer4) 1e-2; layer4 parameter
+norms after each epoch 1e-4 and samples within 2 lr per step taken (AdamW
+moves a weight by ~lr * sign(g), and the sign of near-zero gradients is not
+stable under fp32 reordering); validation loss 1e-3 and identical predictions;
+BatchNorm running-stat sums 1e-3; layer3 weights never stepped.
+"""
+import json
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+
+class _DS:
+    classes = ['Real', 'Class1']
+
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+class _Loader(list):
+    def __init__(self, batches, n_files):
+        super().__init__(batches)
+        self.dataset = _DS(n_files)
+
+
+def _rel(a, b):
+    return abs(a - b) / max(abs(b), 1e-30)
+
+
+def test_trainer_matches_reference_train_fixture():
+    import submodel_trainer as smt
+    from sad import train as st
+    from sad import weights as sw
+    from sad.synth import synth_segment
+    fx = json.load(open(os.path.join(GOLDEN, 'golden_train.json')))
+    labels, seed, files = fx['labels'], fx['seed_pcm'], len(fx['labels'])
+    waves = [[torch.from_numpy(synth_segment(seed, 2 * f + s).astype(np.float32) / 32768.0) for s in range(2)]
+             for f in range(files)]
+    noaug = torch.tensor([0, 0, 0, 0, 0, 0, 512, 512], dtype=torch.int32)
+    batches = []
+    for b in range(files // 2):
+        fs = [2 * b, 2 * b + 1]
+        batches.append((torch.stack([waves[f][0] for f in fs]), torch.tensor([labels[f] for f in fs]),
+                        torch.stack([waves[f][1] for f in fs]), torch.tensor([labels[f] for f in fs]),
+                        noaug.view(1, 1, 8).repeat(2, 2, 1)))
+    loader, val_loader = _Loader(batches, files), _Loader(batches[:1], 2)
+
+    base, head = sw.backbone_state_dict(fx['base_seed']), st.init_state_dict(fx['head_seed'])[1]
+    tr = st.Trainer(base, head, DEV, 'fp32', lr=fx['lr'])
+    model = smt.DeviceModel(tr, st.TrainFrontEnd(DEV, 'fp32'))
+    scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(tr.optimizer, mode='min', factor=0.5, patience=2)
+    l3_before = {n: tr.net.params[n].double().sum().item() for n in fx['layer3_weight_sums']}
+
+    got = []
+    real_step = tr.train_step
+
+    def spy(img, targets, global_batch=None):
+        r = real_step(img, targets, global_batch)
+        torch.cuda.synchronize()
+        got.append({'loss': r[0], 'norm': tr.last_norm[0].item(),
+                    'g': {n: tr.net.grads[n].double().norm().item() for n in tr.net.grads
+                          if n.startswith(('layer3.', 'layer4.'))}})
+        return r
+    tr.train_step = spy
+    args = types.SimpleNamespace(max_steps=0)
+    total_steps = 0
+    epochs = []
+    for epoch in range(2):
+        if epoch == fx['epochs_arg'] // 3:
+            tr.unfreeze_layer3()
+        eloss, eacc, total_steps = smt.train(args, loader, model, None, tr.optimizer, scheduler, epoch,
+                                             smt._Scalars(), total_steps, DEV)
+        epochs.append((eloss, eacc, total_steps, tr.optimizer.param_groups[-1]['lr']))
+        ref_after = fx['steps'][len(got) - 1]['layer4_after']
+        for n, ref in ref_after.items():
+            p = tr.net.params[n].detach().double().cpu()
+            assert _rel(p.norm().item(), ref['norm']) <= 1e-4, (epoch, n)
+            samp = p.flatten()[::max(1, p.numel() // 64)][:64]
+            d = (samp - torch.tensor(ref['sample'], dtype=torch.float64)).abs().max().item()
+            assert d <= 2 * fx['lr'] * len(got) + 1e-5, (epoch, n, d)
+    vloss, vacc, preds, tgts = smt.validate(args, val_loader, model, None, 1, DEV)
+
+    assert len(got) == len(fx['steps']) == 4
+    for i, (g, r) in enumerate(zip(got, fx['steps'])):
+        print(f"step {i}: loss {g['loss']:.6f} vs {r['loss']:.6f}; norm {g['norm']:.6f} vs {r['total_norm']:.6f}")
+        assert _rel(g['loss'], r['loss']) <= 1e-3, i
+        assert _rel(g['norm'], r['total_norm']) <= 2e-3, i
+        assert set(r['grad_norm']) <= set(g['g'])
+        for n, ref in r['grad_norm'].items():
+            assert _rel(g['g'][n], ref) <= 1e-2, (i, n, g['g'][n], ref)
+        # C4: layer3 gradients exist exactly from the unfreeze epoch on
+        assert any(n.startswith('layer3.') for n in r['grad_norm']) == (i >= 2)
+    for (eloss, eacc, steps, lr), ref in zip(epochs, fx['epochs']):
+        assert _rel(eloss, ref['train_loss']) <= 1e-3 and eacc == ref['train_acc']
+        assert steps == ref['total_steps'] and lr == ref['lr']
+    assert _rel(vloss, fx['validate']['loss']) <= 1e-3 and vacc == fx['validate']['acc']
+    assert preds == fx['validate']['preds'] and tgts == fx['validate']['targets']
+    sd = tr.net.base_state_dict()
+    for k, ref in fx['bn_running'].items():
+        assert _rel(sd[f'{k}.running_mean'].double().sum().item(), ref['mean_sum']) <= 1e-3 or \
+            abs(sd[f'{k}.running_mean'].double().sum().item() - ref['mean_sum']) <= 1e-4, k
+        assert _rel(sd[f'{k}.running_var'].double().sum().item(), ref['var_sum']) <= 1e-3, k
+        assert int(sd[f'{k}.num_batches_tracked']) == ref['tracked'], k
+    for n, s in fx['layer3_weight_sums'].items():
+        assert tr.net.params[n].double().sum().item() == l3_before[n]  # never stepped
+        assert _rel(l3_before[n], s) <= 1e-6 or abs(l3_before[n] - s) <= 1e-6

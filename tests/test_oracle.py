@@ -211,3 +211,16 @@ def test_oracle_bottleneck_resnet50_vs_transformers():
         b = hf(x).last_hidden_state
     assert a.shape == b.shape == (2, 2048, 2, 2)
     assert ((a - b).abs().max() / b.abs().max()).item() <= 1e-5
+
+
+def test_segments16_recipe_matches_fixture():
+    """The 16-segment recipe regenerates the PCM the reference fixture was made from."""
+    import os
+    import sys
+    from conftest import GOLDEN
+    sys.path.insert(0, GOLDEN)
+    from make_golden_models16 import segments16
+    pcm = segments16().astype(np.int64)
+    fx = np.load(os.path.join(GOLDEN, 'golden_models16.npz'))
+    assert int(pcm.sum()) == int(fx['pcm_sum'][0]) and int(np.abs(pcm).sum()) == int(fx['pcm_abs_sum'][0])
+    assert fx['n6d_per_head'].shape == (16, 6, 2) and fx['n6d_merged'].shape == (16, 7)
