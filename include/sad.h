@@ -128,6 +128,13 @@ int sad_backbone_run(const sad_backbone_plan* plan, const float* map, int64_t B,
 int sad_backbone_run_img(const sad_backbone_plan* plan, const float* img, int64_t B,
                          int64_t micro_batch, float* feats, void* workspace, size_t ws_bytes,
                          void* stream);
+/* Same from images whose 3 channels may DIFFER: img3 [B, 3, 512, 512] fp32, the
+ * reference's general model input (its load-time check feeds
+ * torch.randn(2,3,512,512), inference_runner.py:119-122 / model_merger.py:
+ * 148-151); conv1 runs per channel in fp32 (not folded), the rest as above. */
+int sad_backbone_run_img3(const sad_backbone_plan* plan, const float* img3, int64_t B,
+                          int64_t micro_batch, float* feats, void* workspace, size_t ws_bytes,
+                          void* stream);
 /* Debug/parity entry: run only the fused resize+stem (conv1+bn1+relu+maxpool)
  * on B maps, writing NHWC [B,128,128,64] in the plan's dtype. */
 int sad_backbone_stem_run(const sad_backbone_plan* plan, const float* map, int64_t B,
@@ -167,6 +174,10 @@ int sad_resnet_run(const sad_resnet_plan* plan, const float* map, int64_t B, int
 /* same from resized images img [B, 512, 512] fp32 (one of the 3 identical channels) */
 int sad_resnet_run_img(const sad_resnet_plan* plan, const float* img, int64_t B, int64_t micro_batch,
                        float* feats, void* workspace, size_t ws_bytes, void* stream);
+
+/* same from [B, 3, 512, 512] fp32 images with possibly distinct channels */
+int sad_resnet_run_img3(const sad_resnet_plan* plan, const float* img3, int64_t B, int64_t micro_batch,
+                        float* feats, void* workspace, size_t ws_bytes, void* stream);
 
 /* Kernel-level timing of the backbone's block-conv launches (bench.py's
  * roofline of the dominant kernel): between begin and end, every block-conv

@@ -63,6 +63,7 @@ struct sad_backbone_plan {
   bool block_path;           // true: persistent block-conv kernels (shortcut in GEMM)
   void* stem_w = nullptr;
   float* stem_b = nullptr;
+  float* stem_w3 = nullptr;    // distinct-channel stem (sad_backbone_run_img3)
   std::vector<DevConv> convs;  // index 1.. of the spec table (igemm path)
   std::vector<DevBlock> blocks;
 };
@@ -139,7 +140,7 @@ int upload_typed(void** dst, const std::vector<double>& v, int dtype, int64_t ro
 
 // conv1 7x7/2 + bn1 folded for the stem kernel, the 3 identical input channels
 // summed; k = ky*7+kx padded to 64 (params: conv weight, BN weight/bias/mean/var)
-int fold_stem(const float* const* params, int dtype, void** w_out, float** b_out) {
+int fold_stem(const float* const* params, int dtype, void** w_out, float** b_out, float** w3_out) {
   const float* W = params[0];
   std::vector<double> sc, sh;
   fold_bn(params[1], params[2], params[3], params[4], 64, sc, sh);
@@ -157,6 +158,12 @@ int fold_stem(const float* const* params, int dtype, void** w_out, float** b_out
     b[co] = (float)sh[co];
   }
   int rc;
+  {  // [64 co][3 c][49 k] fp32, BN scale folded (distinct-channel stem)
+    std::vector<float> w3(64 * 3 * 49);
+    for (int co = 0; co < 64; ++co)
+      for (int i = 0; i < 3 * 49; ++i) w3[co * 147 + i] = (float)((double)W[co * 147 + i] * sc[co]);
+    if ((rc = upload((void**)w3_out, w3))) return rc;
+  }
   if (dtype == SAD_BF16X3) {  // [64 co][64 k] hi, then [64][64] lo
     std::vector<u16> h(2 * 64 * 64);
     for (int i = 0; i < 64 * 64; ++i) {
@@ -190,7 +197,7 @@ extern "C" int sad_backbone_plan_create(const float* const* params, int32_t n_pa
   (void)hipGetDevice(&p->device);
   std::vector<double> sc, sh;
   int rc;
-  if ((rc = fold_stem(params, dtype, &p->stem_w, &p->stem_b))) return rc;
+  if ((rc = fold_stem(params, dtype, &p->stem_w, &p->stem_b, &p->stem_w3))) return rc;
   // first-generation per-conv weights (SAD_BACKBONE_PATH=igemm; fp32 / bf16 only)
   for (size_t ci = 1; ci < specs.size() && dtype != SAD_BF16X3; ++ci) {
     const ConvSpec& s = specs[ci];
@@ -269,6 +276,7 @@ extern "C" int sad_backbone_plan_destroy(sad_backbone_plan* p) {
   if (!p) return SAD_OK;
   (void)hipFree(p->stem_w);
   (void)hipFree(p->stem_b);
+  (void)hipFree(p->stem_w3);
   for (auto& c : p->convs) {
     (void)hipFree(c.w);
     (void)hipFree(c.bias);
@@ -446,7 +454,7 @@ static int front_sub_batch() {
 }
 
 static int run_chunk(const sad_backbone_plan* p, const float* map, const float* img, int64_t mb, float* feats,
-                     void* layer4_out, char* ws, hipStream_t s) {
+                     void* layer4_out, char* ws, hipStream_t s, const float* img3 = nullptr) {
   const size_t ab = act_bytes(p, mb);
   void* bufA = ws;
   void* bufB = ws + ab;
@@ -468,7 +476,7 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
       void* a0 = bufA;
       void* a1 = bufB;
       StemArgs st{map ? map + i * p->mh * p->mw : nullptr, img ? img + i * 512 * 512 : nullptr, p->mh, p->mw,
-                  p->stem_w, p->stem_b, a0, n};
+                  p->stem_w, p->stem_b, a0, n, img3 ? img3 + i * 3 * 512 * 512 : nullptr, p->stem_w3};
       if ((rc = launch_stem(st, p->dtype, s))) return rc;
       H = 128;
       C = 64;
@@ -490,7 +498,7 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
       return rc;
     bufA = a0;
   } else {
-    StemArgs st{map, img, p->mh, p->mw, p->stem_w, p->stem_b, bufA, mb};
+    StemArgs st{map, img, p->mh, p->mw, p->stem_w, p->stem_b, bufA, mb, img3, p->stem_w3};
     if ((rc = launch_stem(st, p->dtype, s))) return rc;
   }
   size_t ci = 0;
@@ -620,6 +628,25 @@ extern "C" int sad_backbone_run_img(const sad_backbone_plan* p, const float* img
   for (int64_t i = 0; i < B; i += mb) {
     const int64_t n = std::min(mb, B - i);
     int rc = run_chunk(p, nullptr, img + i * 512 * 512, n, feats + i * 512, nullptr, (char*)ws, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return SAD_OK;
+}
+
+extern "C" int sad_backbone_run_img3(const sad_backbone_plan* p, const float* img3, int64_t B, int64_t mb,
+                                     float* feats, void* ws, size_t ws_bytes, void* stream) {
+  SAD_REQUIRE(p && img3 && feats && ws, "null args");
+  SAD_REQUIRE(B >= 0 && mb > 0, "bad batch");
+  size_t need = 0;
+  sad_backbone_workspace_size(p, mb, &need);
+  if (ws_bytes < need) {
+    set_error("workspace too small");
+    return SAD_ERR_NOMEM;
+  }
+  for (int64_t i = 0; i < B; i += mb) {
+    const int64_t n = std::min(mb, B - i);
+    int rc = run_chunk(p, nullptr, nullptr, n, feats + i * 512, nullptr, (char*)ws, (hipStream_t)stream,
+                       img3 + i * 3 * 512 * 512);
     if (rc) return rc;
   }
   return SAD_OK;

@@ -723,6 +723,87 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
   }
 }
 
+// ------------------------------------------------- stem, distinct channels --
+// conv1 7x7/2 p3 over 3 DISTINCT input channels (BN scale folded) + bias +
+// ReLU + maxpool 3x3/2 p1, fp32 arithmetic, output in the plan dtype.  The
+// reference's model accepts any [B,3,512,512] tensor (its load-time check feeds
+// torch.randn(2,3,512,512), inference_runner.py:119-122, model_merger.py:
+// 148-151); the spectrogram path's three channels are identical and take the
+// folded MFMA stems above.  Not the hot path: one workgroup per pooled row,
+// one thread per pooled pixel, weights broadcast from LDS.
+// OUT: 0 fp32, 1 bf16, 2 split-bf16 ([hi 32 | lo 32] per 32 channels)
+constexpr int STEM3_PITCH = 520;  // band columns ix + 5 in [0, 519)
+template <int OUT>
+__global__ __launch_bounds__(128) void stem3_kernel(StemArgs a) {
+  __shared__ float s_band[3 * STEM_IMG_ROWS * STEM3_PITCH];
+  __shared__ __attribute__((aligned(16))) float s_w[64 * 148];
+  const int tid = threadIdx.x;
+  const int py = blockIdx.x;
+  const int64_t b = blockIdx.y;
+  for (int i = tid; i < 64 * 147; i += 128) s_w[(i / 147) * 148 + i % 147] = a.w3[i];
+  const float* img = a.img3 + b * 3 * 512 * 512;
+  for (int i = tid; i < 3 * STEM_IMG_ROWS * STEM3_PITCH; i += 128) {
+    const int c = i / (STEM_IMG_ROWS * STEM3_PITCH), r = i % (STEM_IMG_ROWS * STEM3_PITCH);
+    const int tr = r / STEM3_PITCH, tc = r % STEM3_PITCH;
+    const int iy = 4 * py - 5 + tr, ix = tc - 5;
+    s_band[i] = ((unsigned)iy < 512u && (unsigned)ix < 512u) ? img[((int64_t)c * 512 + iy) * 512 + ix] : 0.f;
+  }
+  __syncthreads();
+  const int px = tid;
+  float pooled[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) pooled[j] = 0.f;  // ReLU outputs are >= 0
+  for (int g = 0; g < 4; ++g) {
+    float best[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) best[j] = 0.f;
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int cy = 2 * py + dy;
+      if (cy < 0 || cy >= 256) continue;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int cx = 2 * px + dx;
+        if (cx < 0 || cx >= 256) continue;
+        float acc[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = a.bias[g * 16 + j];
+        for (int c = 0; c < 3; ++c)
+          for (int ky = 0; ky < 7; ++ky) {
+            // band row of image row 2cy - 3 + ky; column 2cx - 3 + kx (+5)
+            const float* br = s_band + (c * STEM_IMG_ROWS + (2 * cy - 3 + ky) - (4 * py - 5)) * STEM3_PITCH + 2 * cx + 2;
+            for (int kx = 0; kx < 7; ++kx) {
+              const float v = br[kx];
+              const float* wr = s_w + (g * 16) * 148 + c * 49 + ky * 7 + kx;
+#pragma unroll
+              for (int j = 0; j < 16; ++j) acc[j] = fmaf(v, wr[j * 148], acc[j]);
+            }
+          }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) best[j] = fmaxf(best[j], acc[j]);  // relu folded into the 0 init
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) pooled[g * 16 + j] = best[j];
+  }
+  const int64_t pix = (b * 128 + py) * 128 + px;
+  if constexpr (OUT == 0) {
+    float* o = (float*)a.out + pix * 64;
+#pragma unroll
+    for (int j = 0; j < 64; j += 4) *(float4*)(o + j) = make_float4(pooled[j], pooled[j + 1], pooled[j + 2], pooled[j + 3]);
+  } else if constexpr (OUT == 1) {
+    u16* o = (u16*)a.out + pix * 64;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) o[j] = f2bf(pooled[j]);
+  } else {
+    u16* o = (u16*)a.out + pix * 128;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      const u16 h = f2bf(pooled[j]);
+      o[(j >> 5) * 64 + (j & 31)] = h;
+      o[(j >> 5) * 64 + 32 + (j & 31)] = f2bf(pooled[j] - bf2f(h));
+    }
+  }
+}
+
 // --------------------------------------------------------------- avgpool --
 // [B, HW, C] (NHWC, dtype T) -> [B, C] fp32 mean over HW.  Workgroup = one
 // segment x 64 channels; 4 waves split the pixels, LDS combine.
@@ -817,6 +898,17 @@ int launch_conv(const ConvArgs& a_in, int dtype, hipStream_t s, int variant) {
 int launch_stem(const StemArgs& a, int dtype, hipStream_t s) {
   SAD_REQUIRE(a.B <= 65535, "stem: B > 65535");
   if (a.B == 0) return SAD_OK;
+  if (a.img3) {
+    SAD_REQUIRE(a.w3 && a.bias, "distinct-channel stem: weights");
+    if (dtype == SAD_F32)
+      hipLaunchKernelGGL(stem3_kernel<0>, dim3(128, (unsigned)a.B), dim3(128), 0, s, a);
+    else if (dtype == SAD_BF16)
+      hipLaunchKernelGGL(stem3_kernel<1>, dim3(128, (unsigned)a.B), dim3(128), 0, s, a);
+    else
+      hipLaunchKernelGGL(stem3_kernel<2>, dim3(128, (unsigned)a.B), dim3(128), 0, s, a);
+    SAD_CHECK_HIP(hipGetLastError());
+    return SAD_OK;
+  }
   if (dtype == SAD_BF16)
     hipLaunchKernelGGL(stem_bf16_kernel<false>, dim3(128 / STEM_P, (unsigned)a.B), dim3(256), 0, s, a);
   else if (dtype == SAD_BF16X3)

@@ -65,6 +65,8 @@ struct StemArgs {
   const float* bias;     // [64]
   void* out;             // NHWC [B, 128, 128, 64]
   int64_t B;
+  const float* img3;     // [B, 3, 512, 512] fp32 images with DISTINCT channels (stem3 kernel), or null
+  const float* w3;       // [64][3][49] fp32 conv1 with bn1's scale folded (the stem3 kernel's weights)
 };
 
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s, int variant = 0);
@@ -90,7 +92,8 @@ void fold_bn(const float* g, const float* beta, const float* mu, const float* va
              std::vector<double>& scale, std::vector<double>& shift);
 // fp32, bf16 (RNE) or split-bf16 (row_len: K per weight row, hi/lo interleaved per 32)
 int upload_typed(void** dst, const std::vector<double>& v, int dtype, int64_t row_len = 0);
-// timm conv1 + bn1 (5 arrays) -> the stem kernel's weight layout and bias
-int fold_stem(const float* const* params, int dtype, void** w_out, float** b_out);
+// timm conv1 + bn1 (5 arrays) -> the stem kernel's weight layout and bias, and
+// (w3_out) the per-channel fp32 weights of the 3-distinct-channel stem
+int fold_stem(const float* const* params, int dtype, void** w_out, float** b_out, float** w3_out);
 
 }  // namespace sad

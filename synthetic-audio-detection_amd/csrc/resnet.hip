@@ -91,6 +91,7 @@ struct sad_resnet_plan {
   int dtype, mh, mw, block, num_features;
   void* stem_w = nullptr;
   float* stem_b = nullptr;
+  float* stem_w3 = nullptr;  // distinct-channel stem (sad_resnet_run_img3)
   std::vector<Block> blocks;
   int64_t max_elems = 0;  // largest activation per segment (elements)
 };
@@ -99,6 +100,7 @@ extern "C" int sad_resnet_plan_destroy(sad_resnet_plan* p) {
   if (!p) return SAD_OK;
   (void)hipFree(p->stem_w);
   (void)hipFree(p->stem_b);
+  (void)hipFree(p->stem_w3);
   for (auto& b : p->blocks) {
     free_conv(b.c1);
     free_conv(b.c2);
@@ -136,7 +138,7 @@ extern "C" int sad_resnet_plan_create(const float* const* params, int32_t n_para
   p->block = block;
   p->num_features = 512 * exp;
   int rc;
-  if ((rc = fold_stem(params, dtype, &p->stem_w, &p->stem_b))) {
+  if ((rc = fold_stem(params, dtype, &p->stem_w, &p->stem_b, &p->stem_w3))) {
     sad_resnet_plan_destroy(p);
     return rc;
   }
@@ -238,14 +240,14 @@ static int rn_block_conv(const sad_resnet_plan* p, const ConvW& c, const void* x
 }
 
 static int rn_chunk(const sad_resnet_plan* p, const float* map, const float* img, int64_t n, float* feats, char* ws,
-                    hipStream_t s) {
+                    hipStream_t s, const float* img3 = nullptr) {
   const size_t ab = rn_act_bytes(p, n);
   void* X = ws;
   void* Y = ws + ab;
   void* T1 = ws + 2 * ab;
   void* T2 = ws + 3 * ab;
   int rc;
-  StemArgs st{map, img, p->mh, p->mw, p->stem_w, p->stem_b, X, n};
+  StemArgs st{map, img, p->mh, p->mw, p->stem_w, p->stem_b, X, n, img3, p->stem_w3};
   if ((rc = launch_stem(st, p->dtype, s))) return rc;
   int H = 128, C = 64;
   for (const Block& b : p->blocks) {
@@ -270,8 +272,8 @@ static int rn_chunk(const sad_resnet_plan* p, const float* map, const float* img
 }
 
 static int rn_run(const sad_resnet_plan* p, const float* map, const float* img, int64_t B, int64_t mb, float* feats,
-                  void* ws, size_t ws_bytes, hipStream_t s) {
-  SAD_REQUIRE(p && (map || img) && feats && ws, "null args");
+                  void* ws, size_t ws_bytes, hipStream_t s, const float* img3 = nullptr) {
+  SAD_REQUIRE(p && (map || img || img3) && feats && ws, "null args");
   SAD_REQUIRE(B >= 0 && mb > 0, "bad batch");
   size_t need = 0;
   sad_resnet_workspace_size(p, mb, &need);
@@ -283,7 +285,7 @@ static int rn_run(const sad_resnet_plan* p, const float* map, const float* img, 
   for (int64_t i = 0; i < B; i += mb) {
     const int64_t n = std::min(mb, B - i);
     int rc = rn_chunk(p, map ? map + i * plane : nullptr, img ? img + i * plane : nullptr, n,
-                      feats + i * p->num_features, (char*)ws, s);
+                      feats + i * p->num_features, (char*)ws, s, img3 ? img3 + i * 3 * 512 * 512 : nullptr);
     if (rc) return rc;
   }
   return SAD_OK;
@@ -299,4 +301,10 @@ extern "C" int sad_resnet_run_img(const sad_resnet_plan* p, const float* img, in
                                   void* ws, size_t ws_bytes, void* stream) {
   SAD_REQUIRE(img, "null img");
   return rn_run(p, nullptr, img, B, mb, feats, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int sad_resnet_run_img3(const sad_resnet_plan* p, const float* img3, int64_t B, int64_t mb, float* feats,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  SAD_REQUIRE(img3, "null img3");
+  return rn_run(p, nullptr, nullptr, B, mb, feats, ws, ws_bytes, (hipStream_t)stream, img3);
 }

@@ -146,12 +146,14 @@ class ModularMultiHeadClassifier:
         x = x.to(self.device, torch.float32)
         if x.dim() != 4 or x.shape[1] != 3 or x.shape[2:] != (512, 512):
             raise ValueError(f'expected [B,3,512,512], got {tuple(x.shape)}')
-        if not (torch.equal(x[:, 0], x[:, 1]) and torch.equal(x[:, 0], x[:, 2])):
-            raise NotImplementedError('the device stem folds the 3 identical spectrogram channels '
-                                      '(inference_runner.py:173); distinct channels are not supported')
-        img = x[:, 0].contiguous()
         eng = self.engine
-        feats = [bb.forward_images(img) for bb in eng.backbones]
+        if torch.equal(x[:, 0], x[:, 1]) and torch.equal(x[:, 0], x[:, 2]):
+            # the spectrogram path (repeat(3), :173): conv1 folded over the channels
+            img = x[:, 0].contiguous()
+            feats = [bb.forward_images(img) for bb in eng.backbones]
+        else:  # any other tensor (e.g. the load-time randn(2,3,512,512) check, :119-122)
+            img3 = x.contiguous()
+            feats = [bb.forward_images3(img3) for bb in eng.backbones]
         return eng.heads(feats)[1]
 
     forward = __call__
@@ -194,9 +196,10 @@ def load_merged_model(merged_path: str, device: torch.device, backbone_name='res
         sm.load_state_dict(local_sd, strict=False)
         sub_models.append(sm)
     final_model = ModularMultiHeadClassifier(sub_models, device, precision)
-    # Quick test (reference :119-122): build the device plans, one dummy forward.
-    dummy = final_model.forward_maps(torch.zeros(2, 128, 251))
-    print('Rebuilt merged model => dummy output shape:', torch.Size([2, dummy.shape[1]]))
+    # Quick test (reference :119-122): build the device plans, one dummy forward
+    # of the reference's own random [2, 3, 512, 512] input (distinct channels).
+    dummy = final_model(torch.randn(2, 3, 512, 512))
+    print('Rebuilt merged model => dummy output shape:', dummy.shape)
     return final_model, metadata
 
 

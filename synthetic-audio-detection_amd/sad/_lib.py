@@ -52,6 +52,7 @@ SIGNATURES = {
     'sad_backbone_workspace_size': (ctypes.c_int, [P, I64, ctypes.POINTER(SZ)]),
     'sad_backbone_run': (ctypes.c_int, [P, P, I64, I64, P, P, SZ, P]),
     'sad_backbone_run_img': (ctypes.c_int, [P, P, I64, I64, P, P, SZ, P]),
+    'sad_backbone_run_img3': (ctypes.c_int, [P, P, I64, I64, P, P, SZ, P]),
     'sad_backbone_stem_run': (ctypes.c_int, [P, P, I64, P, P]),
     'sad_backbone_run_debug': (ctypes.c_int, [P, P, I64, P, P, P, SZ, P]),
     'sad_resnet_plan_create': (ctypes.c_int, [FPP, I32, I32, ctypes.POINTER(I32), I32, I32, I32,
@@ -61,6 +62,7 @@ SIGNATURES = {
     'sad_resnet_workspace_size': (ctypes.c_int, [P, I64, ctypes.POINTER(SZ)]),
     'sad_resnet_run': (ctypes.c_int, [P, P, I64, I64, P, P, SZ, P]),
     'sad_resnet_run_img': (ctypes.c_int, [P, P, I64, I64, P, P, SZ, P]),
+    'sad_resnet_run_img3': (ctypes.c_int, [P, P, I64, I64, P, P, SZ, P]),
     'sad_profile_begin': (ctypes.c_int, []),
     'sad_profile_end': (ctypes.c_int, [I32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(I64),
                                        ctypes.POINTER(ctypes.c_double)]),

@@ -206,6 +206,18 @@ class Backbone:
                       ws.numel(), _lib.stream_handle(self.device))
         return feats
 
+    def forward_images3(self, img3: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """img3 [B,3,512,512] fp32 with possibly distinct channels -> feats [B,512]."""
+        assert img3.dtype == torch.float32 and img3.shape[1:] == (3, 512, 512) and img3.is_contiguous()
+        B = img3.shape[0]
+        feats = out if out is not None else torch.empty(B, 512, device=self.device, dtype=torch.float32)
+        mb = max(1, min(self.micro_batch, B))
+        ws = self.workspace(mb)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_backbone_run_img3', self._plan, _lib.ptr(img3), B, mb, _lib.ptr(feats), _lib.ptr(ws),
+                      ws.numel(), _lib.stream_handle(self.device))
+        return feats
+
     def stem(self, maps: torch.Tensor) -> torch.Tensor:
         """NHWC [B,128,128,64] in the plan dtype (bf16x3: fp32 decoded from the split layout)."""
         B = maps.shape[0]
@@ -278,6 +290,11 @@ class ResNetBackbone:
         """img [B,512,512] fp32 (one channel of the reference's identical three) -> feats."""
         assert img.dtype == torch.float32 and img.shape[1:] == (512, 512) and img.is_contiguous()
         return self._run('sad_resnet_run_img', img, out)
+
+    def forward_images3(self, img3: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """img3 [B,3,512,512] fp32 with possibly distinct channels -> feats."""
+        assert img3.dtype == torch.float32 and img3.shape[1:] == (3, 512, 512) and img3.is_contiguous()
+        return self._run('sad_resnet_run_img3', img3, out)
 
     def __del__(self):
         try:

@@ -342,8 +342,12 @@ def _gather_lists(preds, tgts, model):
 def validate(args, val_loader, model, criterion, epoch, device):
     """Performs one epoch of validation (:316-385)."""
     classes = val_loader.dataset.classes
-    loss_sum, correct, total, preds, tgts = _eval_pass(val_loader, model)
-    preds = [min(max(p, 0), len(classes) - 1) for p in preds]  # :349
+    loss_sum, _, total, preds, tgts = _eval_pass(val_loader, model)
+    # the argmax over the 512 pooled features (quirk C1) is clamped to the class
+    # range BEFORE it is compared with the target (:345-352), so an index > 1
+    # counts as class 1 -- pinned by tests/golden/golden_train.json
+    preds = [min(max(p, 0), len(classes) - 1) for p in preds]
+    correct = sum(int(p == t) for p, t in zip(preds, tgts))
     epoch_loss = loss_sum / len(val_loader.dataset) if len(val_loader.dataset) > 0 else 0.0
     epoch_acc = 100. * correct / total if total > 0 else 0.0
     logging.info(f"Unique targets in validation: {set(tgts)}")
