@@ -303,18 +303,26 @@ int sad_bn_backward_run(const void* x, int64_t P, int32_t C, int32_t dtype, cons
                         const void* dy, const float* dpool, int32_t pool_hw, const void* y, float* dgamma,
                         float* dbeta, int32_t accumulate, void* dz_out, void* dx, float* ws, size_t ws_bytes,
                         void* stream);
-/* Conv weight gradient: dw [Cout][Cin][k][k] fp32 = beta*dw + sum_p dy (x) im2col(x)
- * (im2col into col_ws: N*Ho*Wo*Cin*k*k elements of dtype; not used for 1x1/s1). */
+/* Conv weight gradient (wgrad.hip, hand-written MFMA, no im2col): dw
+ * [Cout][Cin][k][k] fp32 = beta*dw + sum_p dy[p] (x) x[src(p, tap)], the
+ * activation gathered per tap straight from NHWC x; split-K partials in ws
+ * (sad_conv_wgrad_workspace_size bytes), reduced in a fixed order
+ * (deterministic).  Cin, Cout multiples of 8 (bf16) / 4 (fp32). */
+int sad_conv_wgrad_workspace_size(int64_t N, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t k,
+                                  int32_t stride, int32_t pad, int32_t dtype, size_t* bytes);
 int sad_conv_wgrad_run(const void* x, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* dy, int32_t Cout,
-                       int32_t k, int32_t stride, int32_t pad, int32_t dtype, float beta, float* dw, void* col_ws,
+                       int32_t k, int32_t stride, int32_t pad, int32_t dtype, float beta, float* dw, void* ws,
                        size_t ws_bytes, void* stream);
-/* Conv input gradient for any stride: dcol = dy * W (w_oihw from pack mode 3),
- * col2im gather into dx NHWC [N, H, W, Cin] (added to dx if accumulate);
- * col_ws: N*Ho*Wo*Cin*k*k fp32.  (Stride-1 3x3 dgrad runs as sad_conv2d_run
- * over dy with pack mode 1 weights instead.) */
+/* Conv input gradient for any stride (wgrad.hip): dcol[p][j] = sum_co dy[p][co]
+ * W[co][j] on the same MFMA kernel (w_oihw from pack mode 3, dy transposed
+ * into ws), then the col2im gather into dx NHWC [N, H, W, Cin] (added to dx
+ * if accumulate).  ws: sad_conv_dgrad_workspace_size bytes.  (Stride-1 3x3
+ * dgrad runs as a block conv over dy with pack mode 1 weights instead.) */
+int sad_conv_dgrad_workspace_size(int64_t N, int32_t Ho, int32_t Wo, int32_t Cout, int32_t Cin, int32_t k,
+                                  int32_t dtype, size_t* bytes);
 int sad_conv_dgrad_run(const void* dy, int64_t N, int32_t Ho, int32_t Wo, int32_t Cout, const void* w_oihw,
                        int32_t Cin, int32_t H, int32_t W, int32_t k, int32_t stride, int32_t pad, int32_t dtype,
-                       int32_t accumulate, void* dx, float* col_ws, size_t ws_bytes, void* stream);
+                       int32_t accumulate, void* dx, void* ws, size_t ws_bytes, void* stream);
 /* torch.nn.utils.clip_grad_norm_(params, max_norm) over one flat fp32 gradient
  * buffer (:276): norm_coef[0] = ||g||, norm_coef[1] = min(max_norm/(||g||+1e-6), 1);
  * g *= norm_coef[1].  ws >= 1024 doubles. */

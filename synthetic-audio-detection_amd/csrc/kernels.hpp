@@ -76,6 +76,9 @@ int launch_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, int vari
 int default_block_variant(const BlockConvArgs& a, int dtype);
 bool layer2_halo();
 bool block_conv_can_pool(const BlockConvArgs& a, int dtype);  // default variant pools Ho x Wo tiles  // SAD_L2_HALO (default 1): layer2's identity blocks on the halo kernel
+// dx (+)= col2im(dcol) (train.hip; the strided dgrad of wgrad.hip)
+int launch_col2im(const float* dcol, int64_t N, int H, int W, int C, int k, int stride, int pad, int Ho, int Wo,
+                  int accumulate, void* dx, int dtype, hipStream_t s);
 int launch_avgpool(const void* in, int64_t B, int hw, int c, float* out, int dtype, hipStream_t s);
 int launch_heads_final(const float* y2, int64_t B, int n_heads, const float* w3, const float* b3,
                        float* logits, float* merged, hipStream_t s);

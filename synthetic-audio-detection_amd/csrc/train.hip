@@ -18,10 +18,7 @@
 // are plain library GEMMs after im2col (wgrad, strided dgrad), rocBLAS.
 #include <math.h>
 
-#include <mutex>
 #include <vector>
-
-#include <rocblas/rocblas.h>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -553,31 +550,7 @@ __global__ __launch_bounds__(1024) void ce_kernel(const float* __restrict__ z, c
   }
 }
 
-// ------------------------------------------------------------ im2col --
-// col[p][ci*k*k + ky*k + kx] = x[n, oy*s-pad+ky, ox*s-pad+kx, ci] (0 outside):
-// the OIHW-ordered K axis makes the wgrad GEMM write torch's weight layout.
-// Thread = one output pixel x one input channel (k*k consecutive stores).
-template <typename T>
-__global__ void im2col_kernel(const T* __restrict__ x, int H, int W, int C, int k, int s, int pad, int Ho, int Wo,
-                              T* __restrict__ col, int64_t total) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= total) return;
-  const int ci = (int)(idx % C);
-  const int64_t pix = idx / C;
-  const int ox = (int)(pix % Wo), oy = (int)((pix / Wo) % Ho);
-  const int64_t n = pix / ((int64_t)Wo * Ho);
-  const int kk = k * k;
-  T* o = col + pix * ((int64_t)C * kk) + (int64_t)ci * kk;
-  for (int ky = 0; ky < k; ++ky) {
-    const int iy = oy * s - pad + ky;
-    for (int kx = 0; kx < k; ++kx) {
-      const int ix = ox * s - pad + kx;
-      const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
-      o[ky * k + kx] = ok ? x[((n * H + iy) * W + ix) * C + ci] : (T)0;
-    }
-  }
-}
-
+// ------------------------------------------------------------ col2im --
 // Gather form of col2im (deterministic): dx[n,iy,ix,ci] (+)= sum over taps with
 // (iy + pad - ky) % s == 0 of dcol[n,oy,ox][ci*k*k + ky*k + kx].
 template <typename T>
@@ -664,42 +637,22 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   v[i] = vi;
 }
 
-// ------------------------------------------------------------ rocBLAS --
-// One handle per device (created on first use; rocBLAS handles are not
-// thread-safe, so calls are serialised per device).
-struct BlasSlot {
-  rocblas_handle h = nullptr;
-  std::mutex mu;
-};
-static BlasSlot g_blas[64];
-
-static int gemm_ex(int dtype, bool transB, int m, int n, int k, const void* A, int lda, const void* B, int ldb,
-                   float beta, float* C, int ldc, hipStream_t s) {
-  int dev = 0;
-  SAD_CHECK_HIP(hipGetDevice(&dev));
-  SAD_REQUIRE(dev >= 0 && dev < 64, "device index");
-  BlasSlot& slot = g_blas[dev];
-  std::lock_guard<std::mutex> lk(slot.mu);
-  if (!slot.h && rocblas_create_handle(&slot.h) != rocblas_status_success) {
-    set_error("rocblas_create_handle failed");
-    return SAD_ERR_STATE;
-  }
-  rocblas_set_stream(slot.h, s);
-  const float alpha = 1.f;
-  const rocblas_datatype ti = dtype == SAD_BF16 ? rocblas_datatype_bf16_r : rocblas_datatype_f32_r;
-  const rocblas_status st =
-      rocblas_gemm_ex(slot.h, rocblas_operation_none, transB ? rocblas_operation_transpose : rocblas_operation_none, m,
-                      n, k, &alpha, A, ti, lda, B, ti, ldb, &beta, C, rocblas_datatype_f32_r, ldc, C,
-                      rocblas_datatype_f32_r, ldc, rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
-  if (st != rocblas_status_success) {
-    set_error(std::string("rocblas_gemm_ex: ") + rocblas_status_to_string(st));
-    return SAD_ERR_HIP;
-  }
-  return SAD_OK;
-}
-
 static inline unsigned nblk(int64_t total, int t = 256) { return (unsigned)((total + t - 1) / t); }
 static inline size_t ES(int dtype) { return dtype == SAD_BF16 ? 2 : 4; }
+
+int launch_col2im(const float* dcol, int64_t N, int H, int W, int C, int k, int stride, int pad, int Ho, int Wo,
+                  int accumulate, void* dx, int dtype, hipStream_t s) {
+  const int64_t total = N * H * W * (int64_t)C;
+  if (!total) return SAD_OK;
+  if (dtype == SAD_BF16)
+    hipLaunchKernelGGL(col2im_kernel<u16>, dim3(nblk(total)), dim3(256), 0, s, dcol, H, W, C, k, stride, pad, Ho, Wo,
+                       accumulate, (u16*)dx, total);
+  else
+    hipLaunchKernelGGL(col2im_kernel<float>, dim3(nblk(total)), dim3(256), 0, s, dcol, H, W, C, k, stride, pad, Ho,
+                       Wo, accumulate, (float*)dx, total);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
+}
 
 }  // namespace sad
 
@@ -906,59 +859,6 @@ extern "C" int sad_bn_backward_run(const void* x, int64_t P, int32_t C, int32_t 
     hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(nblk(total)), dim3(256), 0, s, (const float*)x, P, C,
                        (const float*)dz_out, (const float*)dy, dpool, pool_hw > 0 ? pool_hw : 1, (const float*)y,
                        stats, coef, (float*)dx);
-  SAD_CHECK_HIP(hipGetLastError());
-  return SAD_OK;
-}
-
-extern "C" int sad_conv_wgrad_run(const void* x, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* dy,
-                                  int32_t Cout, int32_t k, int32_t stride, int32_t pad, int32_t dtype, float beta,
-                                  float* dw, void* col_ws, size_t ws_bytes, void* stream) {
-  SAD_REQUIRE(x && dy && dw && N >= 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && k > 0 && stride > 0, "bad args");
-  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
-  const int Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
-  const int64_t P = N * Ho * Wo, J = (int64_t)Cin * k * k;
-  SAD_REQUIRE(P < (1ll << 31) && J < (1ll << 31), "wgrad too large");
-  hipStream_t s = (hipStream_t)stream;
-  const void* A = x;
-  if (!(k == 1 && stride == 1 && pad == 0)) {
-    SAD_REQUIRE(col_ws && ws_bytes >= (size_t)(P * J) * ES(dtype), "wgrad col workspace too small");
-    const int64_t total = P * Cin;
-    if (dtype == SAD_BF16)
-      hipLaunchKernelGGL(im2col_kernel<u16>, dim3(nblk(total)), dim3(256), 0, s, (const u16*)x, H, W, Cin, k, stride,
-                         pad, Ho, Wo, (u16*)col_ws, total);
-    else
-      hipLaunchKernelGGL(im2col_kernel<float>, dim3(nblk(total)), dim3(256), 0, s, (const float*)x, H, W, Cin, k,
-                         stride, pad, Ho, Wo, (float*)col_ws, total);
-    SAD_CHECK_HIP(hipGetLastError());
-    A = col_ws;
-  }
-  if (P == 0) return SAD_OK;
-  // column-major: dW^T (J x Cout) = col^T (J x P) * dy (P x Cout)
-  return gemm_ex(dtype, true, (int)J, Cout, (int)P, A, (int)J, dy, Cout, beta, dw, (int)J, s);
-}
-
-extern "C" int sad_conv_dgrad_run(const void* dy, int64_t N, int32_t Ho, int32_t Wo, int32_t Cout, const void* w_oihw,
-                                  int32_t Cin, int32_t H, int32_t W, int32_t k, int32_t stride, int32_t pad,
-                                  int32_t dtype, int32_t accumulate, void* dx, float* col_ws, size_t ws_bytes,
-                                  void* stream) {
-  SAD_REQUIRE(dy && w_oihw && dx && col_ws && N >= 0 && Cin > 0 && Cout > 0 && k > 0 && stride > 0, "bad args");
-  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
-  SAD_REQUIRE((H + 2 * pad - k) / stride + 1 == Ho && (W + 2 * pad - k) / stride + 1 == Wo, "shape mismatch");
-  const int64_t P = N * Ho * Wo, J = (int64_t)Cin * k * k;
-  SAD_REQUIRE(ws_bytes >= (size_t)(P * J) * sizeof(float), "dgrad col workspace too small");
-  SAD_REQUIRE(P < (1ll << 31), "dgrad too large");
-  if (P == 0) return SAD_OK;
-  hipStream_t s = (hipStream_t)stream;
-  // column-major: dcol (J x P) = W^T (J x Cout) * dy^T (Cout x P)
-  int rc = gemm_ex(dtype, false, (int)J, (int)P, Cout, w_oihw, (int)J, dy, Cout, 0.f, col_ws, (int)J, s);
-  if (rc) return rc;
-  const int64_t total = N * H * W * (int64_t)Cin;
-  if (dtype == SAD_BF16)
-    hipLaunchKernelGGL(col2im_kernel<u16>, dim3(nblk(total)), dim3(256), 0, s, col_ws, H, W, Cin, k, stride, pad, Ho,
-                       Wo, accumulate, (u16*)dx, total);
-  else
-    hipLaunchKernelGGL(col2im_kernel<float>, dim3(nblk(total)), dim3(256), 0, s, col_ws, H, W, Cin, k, stride, pad,
-                       Ho, Wo, accumulate, (float*)dx, total);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }

@@ -87,6 +87,9 @@ SIGNATURES = {
     'sad_bn_relu_maxpool_run': (ctypes.c_int, [P, I64, I32, I32, I32, I32, P, P, P]),
     'sad_ce_loss_run': (ctypes.c_int, [P, P, I64, I32, ctypes.c_float, P, P, P, P]),
     'sad_bn_backward_run': (ctypes.c_int, [P, I64, I32, I32, P, P, P, P, I32, P, P, P, I32, P, P, P, SZ, P]),
+    'sad_conv_wgrad_workspace_size': (ctypes.c_int, [I64, I32, I32, I32, I32, I32, I32, I32, I32,
+                                                     ctypes.POINTER(SZ)]),
+    'sad_conv_dgrad_workspace_size': (ctypes.c_int, [I64, I32, I32, I32, I32, I32, I32, ctypes.POINTER(SZ)]),
     'sad_conv_wgrad_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, I32, I32, I32, I32, I32, ctypes.c_float, P, P,
                                           SZ, P]),
     'sad_conv_dgrad_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P,

@@ -316,9 +316,9 @@ class TrainNet:
     def _wgrad(self, x, dy, key, grads, k, stride, pad, beta=0.0):
         N, H, W, Cin = x.shape
         cout = dy.shape[-1]
-        P = dy.numel() // cout
-        need = 0 if (k == 1 and stride == 1 and pad == 0) else P * Cin * k * k * self.es
-        ws = self._buf('col', need)
+        sz = _lib.SZ()
+        _lib.call('sad_conv_wgrad_workspace_size', N, H, W, Cin, cout, k, stride, pad, self._dt, _lib.ctypes.byref(sz))
+        ws = self._buf('wgrad', sz.value)
         with torch.cuda.device(self.device):
             _lib.call('sad_conv_wgrad_run', _lib.ptr(x), N, H, W, Cin, _lib.ptr(dy), cout, k, stride, pad, self._dt,
                       float(beta), _lib.ptr(grads[f'{key}.weight']), _lib.ptr(ws), ws.numel(), self._stream())
@@ -326,7 +326,9 @@ class TrainNet:
     def _dgrad_gemm(self, dy, conv, x_shape, k, stride, pad, dx, accumulate):
         N, Ho, Wo, cout = dy.shape
         _, H, W, Cin = x_shape
-        ws = self._buf('dcol', N * Ho * Wo * Cin * k * k * 4)
+        sz = _lib.SZ()
+        _lib.call('sad_conv_dgrad_workspace_size', N, Ho, Wo, cout, Cin, k, self._dt, _lib.ctypes.byref(sz))
+        ws = self._buf('dgrad', sz.value)
         w = self.packed(conv, 3)
         with torch.cuda.device(self.device):
             _lib.call('sad_conv_dgrad_run', _lib.ptr(dy), N, Ho, Wo, cout, _lib.ptr(w), Cin, H, W, k, stride, pad,
