@@ -265,7 +265,9 @@ int sad_crop_resize_run(const float* map, int64_t n, int32_t h, int32_t w, const
                         int32_t dtype, void* img, void* stream);
 /* fp32 OIHW conv weight -> compute layout in dtype.  mode 0: [Cout][k][k][Cin]
  * (forward); 1: [Cin][k][k][Cout] with flipped taps (stride-1 dgrad as a conv of
- * dy); 2: [Cout][64], k = ky*7+kx, input channels summed (stem); 3: OIHW copy. */
+ * dy); 2: [Cout][64], k = ky*7+kx, input channels summed (fp32 stem); 3: OIHW
+ * copy; 4: [Cout][64], k = ky*8+kx (7x7 in an 8x8 grid), channels summed (bf16
+ * training stem). */
 int sad_pack_conv_weight_run(const float* w, int32_t cout, int32_t cin, int32_t k, int32_t mode, int32_t dtype,
                              void* out, void* stream);
 /* timm conv1 7x7/2/p3 WITHOUT bn1 (train-mode BN needs the raw output):
@@ -273,6 +275,16 @@ int sad_pack_conv_weight_run(const float* w, int32_t cout, int32_t cin, int32_t 
  * elements of dtype; w_packed from mode 2. */
 int sad_stem_conv_run(const void* img, int64_t n, int32_t ih, int32_t iw, const void* w_packed, void* col_ws,
                       size_t ws_bytes, void* out, int32_t dtype, void* stream);
+/* bf16 training stem in one pass (conv.hip stem_bf16_kernel<false, true>):
+ * conv1 7x7/2 of the bf16 image with w_packed (pack mode 4), bn1 in train mode
+ * (batch statistics -> stats, running stats updated as sad_bn_stats_run), ReLU,
+ * maxpool 3x3/2 -> out NHWC [n, 128, 128, 64] bf16.  The raw 256x256 conv map
+ * is never stored: the kernel pools sign(gamma) * conv and sums conv, conv^2
+ * per channel.  ws: sad_stem_train_workspace_size bytes. */
+int sad_stem_train_workspace_size(int64_t n, size_t* bytes);
+int sad_stem_train_run(const void* img, int64_t n, const void* w_packed, const float* gamma, const float* beta,
+                       float eps, float momentum, float* running_mean, float* running_var, float* stats, void* out,
+                       void* ws, size_t ws_bytes, void* stream);
 /* Workspace (bytes) of the BN entries for a [P, C] tensor. */
 int sad_bn_workspace_size(int64_t P, int32_t C, size_t* bytes);
 /* BatchNorm2d train-mode statistics of x NHWC [P, C]: stats = [mean | invstd |

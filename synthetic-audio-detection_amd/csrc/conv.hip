@@ -478,8 +478,19 @@ constexpr int stem_u_floats() {
             : STEM_HROWS * 512 + 256;
 }
 
-template <bool X3>
+// TRAIN (the trainer's bf16 stem, submodel_trainer.py:250-255 in model.train()):
+// bn1 normalises with the BATCH statistics of the raw conv, so nothing can be
+// folded before the pass.  The kernel reads the bf16 training image, computes
+// the raw conv y, and max-pools y' = sign(gamma_c) * y (bias and ReLU skipped):
+// with scale = gamma * invstd, sign(gamma) * scale >= 0, so maxpool(relu(bn(y)))
+// == relu(|scale| * maxpool(y') + shift) exactly, applied afterwards by
+// pooled_bn_relu_kernel (train.hip).  Alongside, every conv row this workgroup
+// owns (2*py0 .. 2*py0 + 2P - 1; the carry-in row belongs to the previous one)
+// feeds per-channel sums of y and y^2 -> a.part[workgroup][2][64] (the
+// bn_reduce_kernel partial format) for the batch statistics.
+template <bool X3, bool TRAIN = false>
 __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) {
+  static_assert(!(X3 && TRAIN), "the training stem is bf16");
   constexpr int OPITCH = X3 ? STEM_OPITCH_X3 : STEM_OPITCH;
   __shared__ __attribute__((aligned(16))) u16 s_img[STEM_BAND_ROWS * STEM_BPITCH];
   __shared__ __attribute__((aligned(16))) u16 s_imgl[X3 ? STEM_BAND_ROWS * STEM_BPITCH : 8];
@@ -497,7 +508,9 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
   const int64_t b = blockIdx.y;
   for (int i = tid; i < 64 * 8; i += 256) {  // [64 co][64 k] bf16 -> pitch 72
     const int co = i >> 3, c8 = (i & 7) * 8;
-    *(uint4*)(s_w + co * 72 + c8) = *(const uint4*)((const u16*)a.w + co * 64 + c8);
+    uint4 wv = *(const uint4*)((const u16*)a.w + co * 64 + c8);
+    if (TRAIN && a.bias[co] < 0.f) wv ^= make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);  // y' = -y
+    *(uint4*)(s_w + co * 72 + c8) = wv;
     if constexpr (X3) *(uint4*)(s_wl + co * 72 + c8) = *(const uint4*)((const u16*)a.w + 64 * 64 + co * 64 + c8);
   }
   // band element store: bf16, or the hi/lo pair
@@ -506,12 +519,20 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
     s_img[i] = h;
     if constexpr (X3) s_imgl[i] = f2bf(v - bf2f(h));
   };
-  if (tid < 64) s_bias[tid] = a.bias[tid];
+  if (tid < 64) s_bias[tid] = TRAIN ? (a.bias[tid] < 0.f ? -1.f : 1.f) : a.bias[tid];
   // ---- image band: rows iy = 4*py0 - 5 + tr, cols ix = tc - 3 (zero outside 512x512)
   // every band row a fragment reads, incl. the zero-weight tap row ky = 7
   // (uninitialised LDS could hold NaN, and NaN * 0 is NaN)
   constexpr int NBR = STEM_BAND_ROWS;
-  if (a.img) {
+  if (TRAIN) {
+    for (int i = tid; i < NBR * STEM_BPITCH; i += 256) {
+      const int tr = i / STEM_BPITCH, tc = i - tr * STEM_BPITCH;
+      const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
+      u16 v = 0;
+      if ((unsigned)iy < 512u && (unsigned)ix < 512u) v = a.img16[(b * 512 + iy) * 512 + ix];
+      s_img[i] = v;
+    }
+  } else if (a.img) {
     for (int i = tid; i < NBR * STEM_BPITCH; i += 256) {
       const int tr = i / STEM_BPITCH, tc = i - tr * STEM_BPITCH;
       const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
@@ -648,12 +669,26 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
     }
   };
 
+  // TRAIN: the conv rows of the image (y', sign folded into s_w) feed the statistics
+  float st_s[4] = {0.f, 0.f, 0.f, 0.f}, st_q[4] = {0.f, 0.f, 0.f, 0.f};
+  auto train_row = [&](const f32x4 (&r)[4][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          st_s[j] += r[i][j][e];
+          st_q[j] += r[i][j][e] * r[i][j][e];
+        }
+  };
   f32x4 carry[4][4], cur[4][4];
   conv_row(2 * py0 - 1, carry);
   for (int pi = 0; pi < STEM_P; ++pi) {
     const int py = py0 + pi;
     // vertical max over conv rows 2py-1, 2py, 2py+1 (carry holds 2py-1)
     conv_row(2 * py, cur);
+    if (TRAIN) train_row(cur);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -661,6 +696,7 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
 #pragma unroll
         for (int e = 0; e < 4; ++e) cur[i][j][e] = fmaxf(carry[i][j][e], cur[i][j][e]);
     conv_row(2 * py + 1, carry);
+    if (TRAIN) train_row(carry);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -692,8 +728,8 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
         const float send = fg == 3 ? (i > 0 ? cur[i - 1][j][3] : 0.f) : x[3];
         float left = __int_as_float(__builtin_amdgcn_ds_bpermute(((lane + 48) & 63) << 2, __float_as_int(send)));
         if (i == 0 && fg == 0) left = wave > 0 ? s_edge[(wave - 1) * 64 + j * 16 + fr] : -INFINITY;
-        const float oa = fmaxf(fmaxf(fmaxf(left, x[0]), x[1]) + bias[j], 0.f);
-        const float ob = fmaxf(fmaxf(fmaxf(x[1], x[2]), x[3]) + bias[j], 0.f);
+        const float oa = TRAIN ? fmaxf(fmaxf(left, x[0]), x[1]) : fmaxf(fmaxf(fmaxf(left, x[0]), x[1]) + bias[j], 0.f);
+        const float ob = TRAIN ? fmaxf(fmaxf(x[1], x[2]), x[3]) : fmaxf(fmaxf(fmaxf(x[1], x[2]), x[3]) + bias[j], 0.f);
         const float oa_next = dppf<0x101>(oa);  // row_shl:1 (fr + 1)
         const float ob_prev = dppf<0x111>(ob);  // row_shr:1 (fr - 1)
         // c0 = channel fr & ~1 (value v0), c0 + 1 (value v1) of pooled pixel q
@@ -720,6 +756,30 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
       *(uint4*)(out + idx) = *(const uint4*)(s_out + (idx / PXE) * OPITCH + (idx % PXE) * 2);
     }
     __syncthreads();
+  }
+  if constexpr (TRAIN) {
+    // lanes (fr, fg = 0..3) share channels 16j + fr: fold fg, then the 4 waves
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      st_s[j] += __shfl_xor(st_s[j], 16, 64);
+      st_s[j] += __shfl_xor(st_s[j], 32, 64);
+      st_q[j] += __shfl_xor(st_q[j], 16, 64);
+      st_q[j] += __shfl_xor(st_q[j], 32, 64);
+    }
+    float* red = s_u;  // [4 waves][2][64]
+    if (fg == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        red[wave * 128 + j * 16 + fr] = st_s[j];
+        red[wave * 128 + 64 + j * 16 + fr] = st_q[j];
+      }
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const float v = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]);
+      // sums of y = sign * y' (the sign is its own inverse); squares are sign-free
+      a.part[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 128 + tid] = tid < 64 ? v * s_bias[tid] : v;
+    }
   }
 }
 
@@ -915,6 +975,15 @@ int launch_stem(const StemArgs& a, int dtype, hipStream_t s) {
     hipLaunchKernelGGL(stem_bf16_kernel<true>, dim3(128 / STEM_P, (unsigned)a.B), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(stem_kernel<float>, dim3(128, (unsigned)a.B), dim3(256), 0, s, a);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
+}
+
+int launch_stem_train(const StemArgs& a, hipStream_t s) {
+  SAD_REQUIRE(a.B <= 65535, "stem: B > 65535");
+  SAD_REQUIRE(a.img16 && a.w && a.bias && a.out && a.part, "training stem: null argument");
+  if (a.B == 0) return SAD_OK;
+  hipLaunchKernelGGL((stem_bf16_kernel<false, true>), dim3(128 / STEM_P, (unsigned)a.B), dim3(256), 0, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }

@@ -67,11 +67,16 @@ struct StemArgs {
   int64_t B;
   const float* img3;     // [B, 3, 512, 512] fp32 images with DISTINCT channels (stem3 kernel), or null
   const float* w3;       // [64][3][49] fp32 conv1 with bn1's scale folded (the stem3 kernel's weights)
+  const u16* img16;      // training stem: [B, 512, 512] bf16 image (bias = bn1 gamma, w unfolded)
+  float* part;           // training stem: per-workgroup [2][64] sums of y, y^2
 };
 
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s, int variant = 0);
 int default_conv_variant(const ConvArgs& a);
 int launch_stem(const StemArgs& a, int dtype, hipStream_t s);
+// training stem (bf16): raw conv1 -> sign(gamma)-pooled raw maps + statistic partials
+int launch_stem_train(const StemArgs& a, hipStream_t s);
+constexpr int STEM_TRAIN_PARTS = 16;  // statistic partials per image (128 pooled rows / STEM_P)
 int launch_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, int variant = 0);
 int default_block_variant(const BlockConvArgs& a, int dtype);
 bool layer2_halo();

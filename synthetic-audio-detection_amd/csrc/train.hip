@@ -199,6 +199,7 @@ __global__ void stem_im2col_kernel(const T* __restrict__ img, int ih, int iw, in
 //   1: [Cin][k][k][Cout], taps flipped     (stride-1 dgrad = conv of dy)
 //   2: [Cout][64], k = ky*7+kx, channels summed (stem, the 3 input planes are identical)
 //   3: [Cout][Cin][k][k]                   (dtype convert; strided dgrad GEMM)
+//   4: [Cout][64], k = ky*8+kx (7x7 in an 8x8 grid), channels summed (bf16 training stem)
 template <typename T>
 __global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int k, int mode,
                                    T* __restrict__ out, int64_t total) {
@@ -221,6 +222,11 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int ci
     v = 0.f;
     if (kp < kk)
       for (int c = 0; c < cin; ++c) v += w[((int64_t)co * cin + c) * kk + kp];
+  } else if (mode == 4) {  // idx = co*64 + ky*8 + kx
+    const int ky = (int)((idx >> 3) & 7), kx = (int)(idx & 7), co = (int)(idx >> 6);
+    v = 0.f;
+    if (ky < k && kx < k)
+      for (int c = 0; c < cin; ++c) v += w[((int64_t)co * cin + c) * kk + ky * k + kx];
   } else {
     v = w[idx];
   }
@@ -381,6 +387,21 @@ __global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(const float* __res
   coef[c] = gamma[c] * stats[C + c];
   coef[C + c] = (float)(s / (double)P);
   coef[2 * C + c] = (float)(q / (double)P);
+}
+
+// The training stem's bn1 + ReLU on the sign(gamma)-max-pooled raw conv
+// (conv.hip stem_bf16_kernel<false, true>): out = relu(|scale| * m' + shift).
+__global__ void pooled_bn_relu_kernel(const u16* __restrict__ m, int64_t P, int C, const float* __restrict__ stats,
+                                      u16* __restrict__ out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int G = C >> 3;
+  if (idx >= P * G) return;
+  const int c0 = (int)(idx % G) * 8;
+  float v[8];
+  load8(m + idx * 8, v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = fmaxf(fabsf(stats[2 * C + c0 + e]) * v[e] + stats[3 * C + c0 + e], 0.f);
+  store8(out + idx * 8, v);
 }
 
 // y = act(x*scale + shift [+ res | + res*rscale + rshift]); thread = 8 channels.
@@ -689,10 +710,11 @@ extern "C" int sad_crop_resize_run(const float* map, int64_t n, int32_t h, int32
 
 extern "C" int sad_pack_conv_weight_run(const float* w, int32_t cout, int32_t cin, int32_t k, int32_t mode,
                                         int32_t dtype, void* out, void* stream) {
-  SAD_REQUIRE(w && out && cout > 0 && cin > 0 && k > 0 && mode >= 0 && mode <= 3, "bad args");
+  SAD_REQUIRE(w && out && cout > 0 && cin > 0 && k > 0 && mode >= 0 && mode <= 4, "bad args");
   SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
   SAD_REQUIRE(mode != 2 || k * k <= 64, "stem pack needs k*k <= 64");
-  const int64_t total = mode == 2 ? (int64_t)cout * 64 : (int64_t)cout * cin * k * k;
+  SAD_REQUIRE(mode != 4 || k <= 8, "8x8-grid stem pack needs k <= 8");
+  const int64_t total = mode == 2 || mode == 4 ? (int64_t)cout * 64 : (int64_t)cout * cin * k * k;
   if (dtype == SAD_BF16)
     hipLaunchKernelGGL(pack_weight_kernel<u16>, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, w, cout, cin, k,
                        mode, (u16*)out, total);
@@ -747,6 +769,43 @@ extern "C" int sad_stem_conv_run(const void* img, int64_t n, int32_t ih, int32_t
   a.Cout = 64;
   a.M = pix;
   return launch_block_conv(a, dtype, s);
+}
+
+extern "C" int sad_stem_train_workspace_size(int64_t n, size_t* bytes) {
+  SAD_REQUIRE(bytes && n >= 0, "bad args");
+  *bytes = (size_t)n * 128 * 128 * 64 * 2 + (size_t)n * STEM_TRAIN_PARTS * 128 * sizeof(float);
+  return SAD_OK;
+}
+
+extern "C" int sad_stem_train_run(const void* img, int64_t n, const void* w_packed, const float* gamma,
+                                  const float* beta, float eps, float momentum, float* running_mean,
+                                  float* running_var, float* stats, void* out, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  SAD_REQUIRE(img && w_packed && gamma && beta && stats && out && ws && n >= 0, "bad args");
+  SAD_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "running stats: both or neither");
+  size_t need = 0;
+  sad_stem_train_workspace_size(n, &need);
+  SAD_REQUIRE(ws_bytes >= need, "stem workspace too small (sad_stem_train_workspace_size)");
+  if (n == 0) return SAD_OK;
+  hipStream_t s = (hipStream_t)stream;
+  u16* pooled = (u16*)ws;
+  float* part = (float*)((char*)ws + (size_t)n * 128 * 128 * 64 * 2);
+  StemArgs a{};
+  a.img16 = (const u16*)img;
+  a.w = w_packed;
+  a.bias = gamma;
+  a.out = pooled;
+  a.part = part;
+  a.B = n;
+  int rc = launch_stem_train(a, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(64), dim3(256), 0, s, part, (int)(n * STEM_TRAIN_PARTS),
+                     n * 256 * 256, 64, gamma, beta, eps, momentum, running_mean, running_var, stats);
+  SAD_CHECK_HIP(hipGetLastError());
+  const int64_t P = n * 128 * 128;
+  hipLaunchKernelGGL(pooled_bn_relu_kernel, dim3(nblk(P * 8)), dim3(256), 0, s, pooled, P, 64, stats, (u16*)out);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
 }
 
 static int bn_nblocks(int64_t P, int C) {

@@ -80,6 +80,8 @@ SIGNATURES = {
     'sad_crop_resize_run': (ctypes.c_int, [P, I64, I32, I32, P, I32, I32, P, P]),
     'sad_pack_conv_weight_run': (ctypes.c_int, [P, I32, I32, I32, I32, I32, P, P]),
     'sad_stem_conv_run': (ctypes.c_int, [P, I64, I32, I32, P, P, SZ, P, I32, P]),
+    'sad_stem_train_workspace_size': (ctypes.c_int, [I64, ctypes.POINTER(SZ)]),
+    'sad_stem_train_run': (ctypes.c_int, [P, I64, P, P, P, ctypes.c_float, ctypes.c_float, P, P, P, P, P, SZ, P]),
     'sad_bn_workspace_size': (ctypes.c_int, [I64, I32, ctypes.POINTER(SZ)]),
     'sad_bn_stats_run': (ctypes.c_int, [P, I64, I32, I32, P, P, ctypes.c_float, ctypes.c_float, P, P, P, P, SZ,
                                         P]),

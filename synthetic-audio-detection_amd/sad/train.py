@@ -244,7 +244,7 @@ class TrainNet:
         if t is None:
             w = self.params[f'{conv}.weight']
             co, ci, k, _ = w.shape
-            n = co * 64 if mode == 2 else w.numel()
+            n = co * 64 if mode in (2, 4) else w.numel()
             t = torch.empty(n, device=self.device, dtype=self.tdtype)
             with torch.cuda.device(self.device):
                 _lib.call('sad_pack_conv_weight_run', _lib.ptr(w), co, ci, k, mode, self._dt, _lib.ptr(t),
@@ -341,20 +341,36 @@ class TrainNet:
         assert img.dtype == self.tdtype and img.shape[1:] == (IMG, IMG) and img.is_contiguous()
         B = img.shape[0]
         s = self._stream()
-        raw = torch.empty(B, 256, 256, 64, device=self.device, dtype=self.tdtype)
-        wst = self.packed('conv1', 2)
-        chunk = max(1, min(B, stem_chunk))
-        col = self._buf('stemcol', chunk * 256 * 256 * 64 * self.es)
-        with torch.cuda.device(self.device):
-            for i in range(0, B, chunk):
-                n = min(chunk, B - i)
-                _lib.call('sad_stem_conv_run', _lib.ptr(img[i:i + n]), n, IMG, IMG, _lib.ptr(wst), _lib.ptr(col),
-                          col.numel(), _lib.ptr(raw[i:i + n]), self._dt, s)
-        st = self._bn_stats(raw, 'bn1')
         a = torch.empty(B, 128, 128, 64, device=self.device, dtype=self.tdtype)
-        with torch.cuda.device(self.device):
-            _lib.call('sad_bn_relu_maxpool_run', _lib.ptr(raw), B, 256, 256, 64, self._dt, _lib.ptr(st), _lib.ptr(a), s)
-        del raw
+        if self._dt == _lib.SAD_BF16:
+            # one pass: conv1 + batch statistics + sign(gamma)-max-pool, then bn1 + ReLU
+            # on the pooled map (conv.hip stem_bf16_kernel<false, true>)
+            sz = _lib.SZ()
+            _lib.call('sad_stem_train_workspace_size', B, _lib.ctypes.byref(sz))
+            ws = self._buf('stem', sz.value)
+            st = torch.empty(4 * 64, device=self.device, dtype=torch.float32)
+            rm, rv = self.running['bn1'] if self.update_running else (None, None)
+            with torch.cuda.device(self.device):
+                _lib.call('sad_stem_train_run', _lib.ptr(img), B, _lib.ptr(self.packed('conv1', 4)),
+                          _lib.ptr(self.params['bn1.weight']), _lib.ptr(self.params['bn1.bias']), BN_EPS, BN_MOMENTUM,
+                          _lib.ptr(rm), _lib.ptr(rv), _lib.ptr(st), _lib.ptr(a), _lib.ptr(ws), ws.numel(), s)
+            if self.update_running:
+                self.nbt['bn1'] += 1
+        else:
+            raw = torch.empty(B, 256, 256, 64, device=self.device, dtype=self.tdtype)
+            wst = self.packed('conv1', 2)
+            chunk = max(1, min(B, stem_chunk))
+            col = self._buf('stemcol', chunk * 256 * 256 * 64 * self.es)
+            with torch.cuda.device(self.device):
+                for i in range(0, B, chunk):
+                    n = min(chunk, B - i)
+                    _lib.call('sad_stem_conv_run', _lib.ptr(img[i:i + n]), n, IMG, IMG, _lib.ptr(wst), _lib.ptr(col),
+                              col.numel(), _lib.ptr(raw[i:i + n]), self._dt, s)
+            st = self._bn_stats(raw, 'bn1')
+            with torch.cuda.device(self.device):
+                _lib.call('sad_bn_relu_maxpool_run', _lib.ptr(raw), B, 256, 256, 64, self._dt, _lib.ptr(st),
+                          _lib.ptr(a), s)
+            del raw
         saved = {}
         for prefix, cin, cout, stride, has_ds in self.blocks:
             c1 = self._conv(a, self.packed(f'{prefix}.conv1', 0), cout, 3, stride, 1)
