@@ -285,6 +285,19 @@ int sad_stem_train_workspace_size(int64_t n, size_t* bytes);
 int sad_stem_train_run(const void* img, int64_t n, const void* w_packed, const float* gamma, const float* beta,
                        float eps, float momentum, float* running_mean, float* running_var, float* stats, void* out,
                        void* ws, size_t ws_bytes, void* stream);
+/* Train-mode conv + BatchNorm statistics: out NHWC [N, Ho, Wo, Cout] = raw conv
+ * (no bias) of x with w_packed (pack mode 0), and stats / running stats as
+ * sad_bn_stats_run computes them on out.  bf16 on the block-conv variants 13,
+ * 15, 20 and 25 sums the statistics in the conv epilogue from the fp32
+ * accumulators (out is not re-read; *fused_out = 1); otherwise (fp32, other
+ * shapes) the conv is followed by the bn_reduce pass over out (*fused_out = 0).
+ * ws: sad_conv_bn_train_workspace_size bytes. */
+int sad_conv_bn_train_workspace_size(int64_t N, int32_t H, int32_t W, int32_t Cout, int32_t k, int32_t stride,
+                                     int32_t pad, size_t* bytes);
+int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* w_packed,
+                          int32_t Cout, int32_t k, int32_t stride, int32_t pad, int32_t dtype, const float* gamma,
+                          const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                          float* stats, void* out, float* ws, size_t ws_bytes, int32_t* fused_out, void* stream);
 /* Workspace (bytes) of the BN entries for a [P, C] tensor. */
 int sad_bn_workspace_size(int64_t P, int32_t C, size_t* bytes);
 /* BatchNorm2d train-mode statistics of x NHWC [P, C]: stats = [mean | invstd |
@@ -340,6 +353,19 @@ int sad_conv_dgrad_run(const void* dy, int64_t N, int32_t Ho, int32_t Wo, int32_
  * g *= norm_coef[1].  ws >= 1024 doubles. */
 int sad_clip_grad_norm_run(float* g, int64_t n, float max_norm, float* norm_coef, void* ws, size_t ws_bytes,
                            void* stream);
+/* One conv weight inside the flat parameter buffer and its cached compute
+ * copies (pack modes 0 / 1, either may be NULL) for sad_adamw_pack_run. */
+typedef struct {
+  int64_t offset; /* element offset of the OIHW weight in p */
+  int32_t cout, cin, k, reserved;
+  void* mode0;    /* [Cout][k][k][Cin] in dtype, or NULL */
+  void* mode1;    /* [Cin][k][k][Cout], taps flipped, or NULL */
+} sad_pack_seg;
+/* sad_adamw_run + the updated conv weights written into their packed copies
+ * (<= 16 segments): the trainer's next step needs no pack launches. */
+int sad_adamw_pack_run(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                       float eps, float weight_decay, int64_t step, const sad_pack_seg* segs, int32_t nseg,
+                       int32_t dtype, void* stream);
 /* torch.optim.AdamW step `step` (1-based) over flat fp32 buffers (:648-652,278). */
 int sad_adamw_run(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                   float eps, float weight_decay, int64_t step, void* stream);

@@ -79,6 +79,11 @@ constexpr int block_smem_bytes() {
   return block_ring_bytes<WC, WP, TC, TP, S>() + (block_lds_bias<WC, WP, TC, TP, S, OCC>() ? 16 * TC * WC * 4 : 0) +
          (block_can_pool<WC, WP, TC, TP, S, OCC>() ? 16 * TC * WC * 4 * WP : 0);
 }
+// ST instantiations: + the fused BN statistics, fp32 [WP][2][BC] behind the rest
+template <int WC, int WP, int TC, int TP, int S, int OCC>
+constexpr int block_smem_bytes_st() {
+  return block_smem_bytes<WC, WP, TC, TP, S, OCC>() + WP * 2 * 16 * TC * WC * 4;
+}
 
 // RES: the epilogue adds a residual tensor (a Bottleneck's identity shortcut,
 // resnet.hip) -- its own instantiation, so the ResNet-18 kernels' register
@@ -91,7 +96,9 @@ constexpr int block_smem_bytes() {
 // dropped W_lo.X_lo is ~2^-18 relative), accumulated in fp32; the epilogue
 // splits the fp32 result again.  An identity shortcut (W_hi = I, W_lo = 0)
 // adds X_hi + X_lo exactly.
-template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES, bool X3 = false>
+// ST: training forward (bf16) -- the epilogue also sums the conv output and its
+// square per channel (StatAcc), one [2][BC] row per pixel-group workgroup wi.
+template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES, bool X3 = false, bool ST = false>
 __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_kernel(BlockConvArgs a) {
   static_assert(S == 2 || S == 3, "ring depth");
   static_assert(!X3 || sizeof(T) == 2, "split-bf16 operands are bf16");
@@ -118,8 +125,11 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   const int M = (int)a.M;
   const int tiles_p = (M + BP - 1) / BP;
   const int tp_begin = (int)((int64_t)wi * tiles_p / gp), tp_end = (int)((int64_t)(wi + 1) * tiles_p / gp);
-  if (tp_begin >= tp_end) return;  // whole workgroup (uniform)
   const int c0 = tc * BC;
+  if (tp_begin >= tp_end) {  // whole workgroup (uniform)
+    if constexpr (ST) stat_rows_zero(BC, a.st_part, wi, a.Cout, c0, tid, 64 * NW);
+    return;
+  }
 
   const int nk0 = a.KH * a.KW * a.Cin * ES / 128;
   const int nk1 = a.in1 ? a.Cin1 * ES / 128 : 0;
@@ -231,6 +241,10 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   for (int i = 0; i < TC; ++i)
 #pragma unroll
     for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // ST: [WP][2][BC] fp32 statistics in LDS (register-parked sums spill here)
+  float* s_stat = (float*)(smem + block_smem_bytes<WC, WP, TC, TP, S, OCC>());
+  if constexpr (ST)
+    for (int c = tid; c < WP * 2 * BC; c += 64 * NW) s_stat[c] = 0.f;
 
   const int fr = lane & 15, fg = lane >> 4;
   issue(0);
@@ -394,6 +408,30 @@ if constexpr (X3) {
       float4 bias[TC];
 #pragma unroll
       for (int i = 0; i < TC; ++i) bias[i] = *(const float4*)(s_bias + wc * 16 * TC + i * 16 + fg * 4);
+      if constexpr (ST) {
+#pragma unroll
+        for (int i = 0; i < TC; ++i) {
+          const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float sv = 0.f, qv = 0.f;
+#pragma unroll
+            for (int j = 0; j < TP; ++j) {
+              const int px = ctile * BP + wp * 16 * TP + j * 16 + fr;
+              const float v = px < M ? acc[i][j][r] + bb[r] : 0.f;
+              sv += v;
+              qv += v * v;
+            }
+            sv = row16_sum(sv);
+            qv = row16_sum(qv);
+            if (fr == 0) {
+              const int cl = wc * 16 * TC + i * 16 + fg * 4 + r;
+              s_stat[(wp * 2 + 0) * BC + cl] += sv;
+              s_stat[(wp * 2 + 1) * BC + cl] += qv;
+            }
+          }
+        }
+      }
       if constexpr (POOL_OK) {
         if (a.pool_out) {
           // fused global average pool (the backbone's last conv; a tile = one
@@ -519,21 +557,34 @@ if constexpr (X3) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (ST) {  // fold the WP pixel waves of each channel
+    __syncthreads();
+    stat_rows_write(s_stat, WP, BC, a.st_part, wi, a.Cout, c0, tid, 64 * NW);
+  }
 }
 
-template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES_OK = false, bool X3 = false>
+template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES_OK = false, bool X3 = false,
+          bool ST_OK = false>
 static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
-  constexpr int smem = block_smem_bytes<WC, WP, TC, TP, S, OCC>();
-  static_assert(smem * OCC <= 160 * 1024, "LDS budget");
+  constexpr int smem0 = block_smem_bytes<WC, WP, TC, TP, S, OCC>();
+  static_assert(smem0 * OCC <= 160 * 1024, "LDS budget");
+  static_assert(!ST_OK || block_smem_bytes_st<WC, WP, TC, TP, S, OCC>() * OCC <= 160 * 1024, "LDS budget (ST)");
+  const int smem = a.st_part ? block_smem_bytes_st<WC, WP, TC, TP, S, OCC>() : smem0;
   SAD_REQUIRE(RES_OK || !a.res, "this block-conv variant has no epilogue residual (variants 13, 20, 21, 25 do)");
   const void* kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3>;
   if constexpr (RES_OK) {
     if (a.res) kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true, X3>;
   }
-  static bool attr[2] = {false, false};
-  if (!attr[a.res != nullptr]) {
+  if constexpr (ST_OK) {
+    if (a.st_part) kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3, true>;
+  }
+  SAD_REQUIRE(!a.st_part || (ST_OK && !a.res && !a.pool_out && a.st_rows),
+              "fused BN statistics: variants 13 / 15 (bf16), no residual or pool, st_rows set");
+  static bool attr[3] = {false, false, false};
+  const int ak = a.st_part ? 2 : a.res != nullptr;
+  if (!attr[ak]) {
     (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr[a.res != nullptr] = true;
+    attr[ak] = true;
   }
   constexpr int BC = 16 * TC * WC, BP = 16 * TP * WP;
   const int occupancy = OCC;
@@ -550,6 +601,15 @@ static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
   const int64_t nk = (int64_t)a.KH * a.KW * a.Cin * sizeof(T) / 128 + (a.in1 ? a.Cin1 * sizeof(T) / 128 : 0);
   SAD_REQUIRE(a.M + BP < (1ll << 31) && (tiles_p / (g / n_tc) + 1) * nk < (1ll << 31),
               "block conv: too many pixels for one launch (lower the micro-batch)");
+  if constexpr (ST_OK) {
+    if (a.st_part) {
+      *a.st_rows = (int)(g / n_tc);
+      hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3, true>), dim3((unsigned)g),
+                         dim3(64 * WC * WP), smem, s, a);
+      SAD_CHECK_HIP(hipGetLastError());
+      return SAD_OK;
+    }
+  }
   if constexpr (RES_OK) {
     if (a.res) {
       hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true, X3>), dim3((unsigned)g),
@@ -577,9 +637,9 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
     case 10: return launch_block_t<T, 2, 2, 4, 4, 2, 2, false, X3>(a, s);
     case 11: return launch_block_t<T, 1, 4, 4, 4, 3, 1, false, X3>(a, s);
     case 12: return launch_block_t<T, 2, 2, 4, 4, 3, 1, false, X3>(a, s);
-    case 13: return launch_block_t<T, 2, 4, 8, 4, 2, 1, true, X3>(a, s);
+    case 13: return launch_block_t<T, 2, 4, 8, 4, 2, 1, true, X3, sizeof(T) == 2 && !X3>(a, s);
     case 14: return launch_block_t<T, 2, 4, 4, 4, 2, 1, false, X3>(a, s);
-    case 15: return launch_block_t<T, 2, 4, 4, 4, 3, 1, false, X3>(a, s);
+    case 15: return launch_block_t<T, 2, 4, 4, 4, 3, 1, false, X3, sizeof(T) == 2 && !X3>(a, s);
     case 16: return launch_block_t<T, 1, 8, 4, 4, 2, 1, false, X3>(a, s);
     case 17: return launch_block_t<T, 2, 2, 8, 4, 2, 1, false, X3>(a, s);
     case 18: return launch_block_t<T, 2, 2, 4, 8, 2, 1, false, X3>(a, s);
@@ -622,13 +682,30 @@ static int c128_variant() {
   }();
   return v;
 }
+static int block_device_cus() {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    cus[dev] = c;
+  }
+  return cus[dev];
+}
 int default_block_variant(const BlockConvArgs& a, int dtype) {
   // split-bf16: the halo kernel for the stride-1 convs of layer1 (Cout 64) and
   // layer2 (Cout 128), whose implicit GEMM is L2->LDS-fill bound
   if (dtype == SAD_BF16X3) return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
   if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo()))) return 20;
-  return a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9);
+  // small maps (the trainer's 64-segment layer4: M = 16384): 256x256 tiles would
+  // leave CUs idle (one workgroup per CU), so split the channel tile (variant
+  // 15, 128x256).  Both keep the 256-pixel tile and the same K order, so the
+  // results (incl. the fused average pool) do not depend on the choice.
+  if (a.Cout % 256 == 0)
+    return a.res || (a.M + 255) / 256 * (a.Cout / 256) >= block_device_cus() ? 13 : 15;  // 13: residual epilogue
+  return a.Cout % 128 == 0 ? c128_variant() : 9;
 }
 // pixel tile of the variants that can fuse the average pool (0: cannot)
 static int pool_tile(int v) {

@@ -94,7 +94,9 @@ struct HaloGeo {
 // chunk, so a K-step's halves are hi and lo; three MFMA sets per step; the
 // epilogue adds the residual (hi + lo, loaded into registers during the
 // tile's last chunk) and stores hi/lo from registers.
-template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU, bool X3 = false>
+// ST: training forward -- fused BN statistics of the conv output (StatAcc),
+// one [2][BC] row per pixel-group workgroup
+template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU, bool X3 = false, bool ST = false>
 __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(BlockConvArgs a) {
   using G = HaloGeo<WC, WP, TC, TP, TW, X3>;
   constexpr int NL = G::NL, BC = G::BC, TH = G::TH, PW = G::PW, PR = G::PR;
@@ -113,8 +115,11 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
   const int tiles_x = a.W / TW, tiles_img = tiles_x * (a.H / TH);
   const int tiles_p = a.N * tiles_img;
   const int tp_begin = (int)((int64_t)wi * tiles_p / gp), tp_end = (int)((int64_t)(wi + 1) * tiles_p / gp);
-  if (tp_begin >= tp_end) return;
   const int c0 = tc * BC;
+  if (tp_begin >= tp_end) {
+    if constexpr (ST) stat_rows_zero(BC, a.st_part, wi, a.Cout, c0, tid, 64 * WC * WP);
+    return;
+  }
   const int nc0 = a.Cin / 64;  // 64-channel chunks, 9 taps each
 
   const __amdgpu_buffer_rsrc_t r0 =
@@ -202,6 +207,8 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
     for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fg = lane >> 4;
+  StatLane<ST ? TC : 1> stat;
+  stat.zero();
   // fragment j of this wave = tile row ty = wp*TP + j, pixels fr = 0..15
   // epilogue, part 1 (every wave, tap 0 of the next tile): bias [+ residual],
   // activation, bf16 -> the tile's LDS staging rows (in place over the
@@ -261,6 +268,14 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
     }
   };
   auto epilogue = [&]() __attribute__((always_inline)) {
+    if constexpr (ST) {  // statistics of the conv output (bias added, before any residual)
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < TP; ++j) stat.add(i, r, acc[i][j][r] + bias[i][r]);
+    }
     // every residual read issued before the first in-place write (the compiler
     // cannot prove the lanes' read and write addresses disjoint across (i, j))
     uint2 rvs[TP][TC];
@@ -453,6 +468,12 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (!wloader) store_tile(tp_end - 1);
+  if constexpr (ST) {  // patch buffer 0 is free: fold the WP pixel waves of each channel
+    float* s_red = (float*)smem;
+    stat.park(s_red, wp, BC, wc * 16 * TC, fr, fg);
+    __syncthreads();
+    stat_rows_write(s_red, WP, BC, a.st_part, wi, a.Cout, c0, tid, 64 * WC * WP);
+  }
 }
 
 
@@ -472,7 +493,7 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
 // waves 0-3 run theirs before the tile barrier, waves 4-7 after it, so one
 // wave's VALU epilogue overlaps its partner's MFMAs instead of idling the
 // SIMD's matrix pipe.
-template <bool RES, bool RELU>
+template <bool RES, bool RELU, bool ST = false>
 __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
   constexpr int NW = 8, TC = 4, TP = 2, TW = 16, TH = 16;
   constexpr int PW = TW + 2, PR = PW * (TH + 2);  // 18 x 18 patch rows
@@ -490,7 +511,10 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
   const int tiles_x = a.W / TW, tiles_img = tiles_x * (a.H / TH);
   const int tiles_p = a.N * tiles_img;
   const int tp_begin = (int)((int64_t)w * tiles_p / gridDim.x), tp_end = (int)((int64_t)(w + 1) * tiles_p / gridDim.x);
-  if (tp_begin >= tp_end) return;
+  if (tp_begin >= tp_end) {
+    if constexpr (ST) stat_rows_zero(64, a.st_part, w, 64, 0, tid, 512);
+    return;
+  }
 
   const __amdgpu_buffer_rsrc_t r0 =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
@@ -545,6 +569,8 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
   uint2 resv[TC][TP];
 
   const int fr = lane & 15, fg = lane >> 4;
+  StatLane<ST ? TC : 1> stat;
+  stat.zero();
   // lane's pixel of fragment j: tile row 2wp + j, column fr; channels i*16 + fg*4 .. +3
   auto pix_index = [&](int t, int j) __attribute__((always_inline)) {
     const int b = t / tiles_img, rem = t - b * tiles_img;
@@ -559,6 +585,14 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
     }
   };
   auto epilogue = [&](int t) __attribute__((always_inline)) {
+    if constexpr (ST) {  // statistics of the conv output (bias added, before any residual)
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < TP; ++j) stat.add(i, r, acc[i][j][r] + bias[i][r]);
+    }
 #pragma unroll
     for (int j = 0; j < TP; ++j) {
       u16* op = (u16*)a.out + pix_index(t, j) * a.out_pstride + fg * 4;
@@ -660,15 +694,22 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
     pb ^= 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (ST) {  // the resident weights are done: fold the 8 pixel waves
+    __syncthreads();
+    float* s_red = (float*)smem;
+    stat.park(s_red, wp, 64, 0, fr, fg);
+    __syncthreads();
+    stat_rows_write(s_red, NW, 64, a.st_part, w, 64, 0, tid, 512);
+  }
 }
 
-template <bool RES, bool RELU>
+template <bool RES, bool RELU, bool ST = false>
 static int launch_halo_rw_t(const BlockConvArgs& a, hipStream_t s) {
   constexpr int smem = 9 * 64 * 128 + 2 * 41 * 1024;
   static_assert(smem <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)halo_rw_kernel<RES, RELU>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)halo_rw_kernel<RES, RELU, ST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               smem);
     attr = true;
   }
@@ -683,23 +724,29 @@ static int launch_halo_rw_t(const BlockConvArgs& a, hipStream_t s) {
   SAD_REQUIRE(tiles_p < (1ll << 31) && (int64_t)a.N * a.H * a.W * a.in0_pstride * 2 < (1ll << 31),
               "too large for one launch");
   const int64_t g = std::min<int64_t>(tiles_p, 256);
-  hipLaunchKernelGGL((halo_rw_kernel<RES, RELU>), dim3((unsigned)g), dim3(512), smem, s, a);
+  if (ST) *a.st_rows = (int)g;
+  hipLaunchKernelGGL((halo_rw_kernel<RES, RELU, ST>), dim3((unsigned)g), dim3(512), smem, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }
 
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s) {
+  if (a.st_part) {
+    SAD_REQUIRE(!a.res && !a.relu && a.st_rows, "fused BN statistics: raw conv (no residual / ReLU), st_rows set");
+    return launch_halo_rw_t<false, false, true>(a, s);
+  }
   if (a.res) return a.relu ? launch_halo_rw_t<true, true>(a, s) : launch_halo_rw_t<true, false>(a, s);
   return a.relu ? launch_halo_rw_t<false, true>(a, s) : launch_halo_rw_t<false, false>(a, s);
 }
 
-template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU, bool X3>
+template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU, bool X3, bool ST = false>
 static int launch_halo_t(const BlockConvArgs& a, hipStream_t s) {
   using G = HaloGeo<WC, WP, TC, TP, TW, X3>;
   static_assert(G::SMEM <= 160 * 1024, "LDS budget");
+  static_assert(!ST || 2 * G::BC * WP * 4 <= 2 * G::PATCH, "statistics fold area");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)halo_conv_kernel<WC, WP, TC, TP, TW, RES, RELU, X3>,
+    (void)hipFuncSetAttribute((const void*)halo_conv_kernel<WC, WP, TC, TP, TW, RES, RELU, X3, ST>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
     attr = true;
   }
@@ -716,7 +763,8 @@ static int launch_halo_t(const BlockConvArgs& a, hipStream_t s) {
   int64_t g = std::min<int64_t>(tiles_p * n_tc, 256);
   g = std::max<int64_t>(n_tc, g / n_tc * n_tc);
   if (X3) SAD_REQUIRE(a.out_pstride % 64 == 0 && (!a.res || a.res_pstride % 64 == 0), "split-bf16 pixel strides");
-  hipLaunchKernelGGL((halo_conv_kernel<WC, WP, TC, TP, TW, RES, RELU, X3>), dim3((unsigned)g), dim3(64 * WC * WP),
+  if (ST) *a.st_rows = (int)(g / n_tc);
+  hipLaunchKernelGGL((halo_conv_kernel<WC, WP, TC, TP, TW, RES, RELU, X3, ST>), dim3((unsigned)g), dim3(64 * WC * WP),
                      G::SMEM, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
@@ -737,6 +785,11 @@ int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s, bool x3) {
   if (x3) {
     SAD_REQUIRE(v == 20, "split-bf16 halo conv: variant 20");
     return launch_halo_g<1, 8, 4, 2, 16, true>(a, s);
+  }
+  if (a.st_part) {
+    SAD_REQUIRE(v == 20 && !a.res && !a.relu && a.st_rows,
+                "fused BN statistics: halo variant 20, raw conv (no residual / ReLU), st_rows set");
+    return launch_halo_t<1, 8, 4, 2, 16, false, false, false, true>(a, s);
   }
   switch (v) {
     case 20: return launch_halo_g<1, 8, 4, 2, 16>(a, s);

@@ -52,6 +52,9 @@ struct BlockConvArgs {
   float* pool_out;       // optional fused global average pool, fp32 [N, Cout] (the variant's pixel tile
                          // must be one image: block_conv_can_pool); out may then be null
   uint64_t* stamps;      // diagnostic builds only (-DSAD_STAMPS): s_memtime stamps per K-step
+  float* st_part;        // training (bf16): fused BN statistics, fp32 [rows][2][Cout] sums of the
+                         // conv output and its square per workgroup row (variants 13, 15, 20, 25)
+  int* st_rows;          // host out: rows written to st_part by the launch
 };
 
 struct StemArgs {

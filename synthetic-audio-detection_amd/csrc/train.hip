@@ -771,6 +771,24 @@ extern "C" int sad_stem_conv_run(const void* img, int64_t n, int32_t ih, int32_t
   return launch_block_conv(a, dtype, s);
 }
 
+static int bn_nblocks(int64_t P, int C) {
+  const int R = 256 / (C / 8);
+  const int64_t want = (P + R * 16 - 1) / (R * 16);  // >= 16 rows per thread
+  return (int)std::max<int64_t>(1, std::min<int64_t>(1024, want));
+}
+
+// Zero conv bias (the trainer's convs are bias-free; the conv kernels add one)
+static const float* device_zero_bias() {
+  static float* zb[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!zb[dev]) {
+    if (hipMalloc((void**)&zb[dev], 2048 * sizeof(float)) != hipSuccess) return nullptr;
+    if (hipMemset(zb[dev], 0, 2048 * sizeof(float)) != hipSuccess) return nullptr;
+  }
+  return zb[dev];
+}
+
 extern "C" int sad_stem_train_workspace_size(int64_t n, size_t* bytes) {
   SAD_REQUIRE(bytes && n >= 0, "bad args");
   *bytes = (size_t)n * 128 * 128 * 64 * 2 + (size_t)n * STEM_TRAIN_PARTS * 128 * sizeof(float);
@@ -808,10 +826,84 @@ extern "C" int sad_stem_train_run(const void* img, int64_t n, const void* w_pack
   return SAD_OK;
 }
 
-static int bn_nblocks(int64_t P, int C) {
-  const int R = 256 / (C / 8);
-  const int64_t want = (P + R * 16 - 1) / (R * 16);  // >= 16 rows per thread
-  return (int)std::max<int64_t>(1, std::min<int64_t>(1024, want));
+
+// conv -> raw NHWC output + train-mode BatchNorm statistics.  bf16: the
+// statistics are summed in the conv kernels' epilogues (variants 13, 15, 20,
+// 25: StatAcc, one partial row per pixel-group workgroup), so the raw output is
+// never re-read; other shapes / fp32: conv, then the bn_reduce pass.
+static constexpr int kStatRowsMax = 512;  // >= the workgroup rows of any variant (256 x occupancy)
+
+extern "C" int sad_conv_bn_train_workspace_size(int64_t N, int32_t H, int32_t W, int32_t Cout, int32_t k,
+                                                int32_t stride, int32_t pad, size_t* bytes) {
+  SAD_REQUIRE(bytes && N >= 0 && H > 0 && W > 0 && Cout > 0 && k > 0 && stride > 0 && pad >= 0, "bad args");
+  const int64_t P = N * ((H + 2 * pad - k) / stride + 1) * ((W + 2 * pad - k) / stride + 1);
+  const size_t fused = (size_t)kStatRowsMax * 2 * Cout * sizeof(float) + 3 * (size_t)Cout * sizeof(float);
+  const size_t unfused = (size_t)bn_nblocks(P, Cout) * 2 * Cout * sizeof(float) + 3 * (size_t)Cout * sizeof(float);
+  *bytes = std::max(fused, unfused);
+  return SAD_OK;
+}
+
+extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* w_packed,
+                                     int32_t Cout, int32_t k, int32_t stride, int32_t pad, int32_t dtype,
+                                     const float* gamma, const float* beta, float eps, float momentum,
+                                     float* running_mean, float* running_var, float* stats, void* out, float* ws,
+                                     size_t ws_bytes, int32_t* fused_out, void* stream) {
+  SAD_REQUIRE(x && w_packed && gamma && beta && stats && out && ws, "null tensor");
+  SAD_REQUIRE(N > 0 && H > 0 && W > 0 && Cin > 0 && k > 0 && stride > 0 && pad >= 0, "bad shape");
+  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
+  SAD_REQUIRE(Cout % 8 == 0 && Cout >= 8 && Cout <= 2048, "Cout must be a multiple of 8 in [8, 2048]");
+  SAD_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "running stats: both or neither");
+  size_t need = 0;
+  sad_conv_bn_train_workspace_size(N, H, W, Cout, k, stride, pad, &need);
+  SAD_REQUIRE(ws_bytes >= need, "workspace too small (sad_conv_bn_train_workspace_size)");
+  hipStream_t s = (hipStream_t)stream;
+  const float* zb = device_zero_bias();
+  SAD_REQUIRE(zb != nullptr, "zero bias allocation");
+  BlockConvArgs a{};
+  a.in0 = x;
+  a.in0_pstride = Cin;
+  a.N = (int)N;
+  a.H = H;
+  a.W = W;
+  a.Cin = Cin;
+  a.KH = a.KW = k;
+  a.stride = stride;
+  a.pad = pad;
+  a.wt = w_packed;
+  a.bias = zb;
+  a.out = out;
+  a.out_pstride = Cout;
+  a.Ho = (H + 2 * pad - k) / stride + 1;
+  a.Wo = (W + 2 * pad - k) / stride + 1;
+  a.Cout = Cout;
+  a.M = N * a.Ho * a.Wo;
+  const int64_t P = a.M;
+  const int v = default_block_variant(a, dtype);
+  const bool fused = dtype == SAD_BF16 && (v == 13 || v == 15 || v == 20 || v == 25);
+  int rows = 0;
+  if (fused) {
+    a.st_part = ws;
+    a.st_rows = &rows;
+  }
+  int rc = launch_block_conv(a, dtype, s, v);
+  if (rc) return rc;
+  if (fused_out) *fused_out = fused;
+  if (!fused) {
+    const int nb = bn_nblocks(P, Cout);
+    if (dtype == SAD_BF16)
+      hipLaunchKernelGGL((bn_reduce_kernel<u16, 0>), dim3(nb), dim3(256), 0, s, (const u16*)out, P, Cout, nullptr,
+                         nullptr, 1, nullptr, nullptr, nullptr, ws);
+    else
+      hipLaunchKernelGGL((bn_reduce_kernel<float, 0>), dim3(nb), dim3(256), 0, s, (const float*)out, P, Cout,
+                         nullptr, nullptr, 1, nullptr, nullptr, nullptr, ws);
+    SAD_CHECK_HIP(hipGetLastError());
+    rows = nb;
+  }
+  SAD_REQUIRE(rows > 0 && rows <= kStatRowsMax, "statistic partial rows");
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(Cout), dim3(256), 0, s, ws, rows, P, Cout, gamma, beta, eps,
+                     momentum, running_mean, running_var, stats);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
 }
 
 extern "C" int sad_bn_workspace_size(int64_t P, int32_t C, size_t* bytes) {
@@ -956,6 +1048,66 @@ extern "C" int sad_avgpool_run(const void* x, int64_t B, int32_t hw, int32_t C, 
                                void* stream) {
   SAD_REQUIRE(x && out && B >= 0 && hw > 0 && C % 64 == 0, "bad args (C must be a multiple of 64)");
   return launch_avgpool(x, B, hw, C, out, dtype, (hipStream_t)stream);
+}
+
+// AdamW + re-pack of the updated conv weights into their cached compute
+// layouts (pack modes 0 and 1), so the next forward / backward needs no pack
+// launches.  Segment search is per thread over <= 16 (wave-uniform) entries.
+struct PackSegs {
+  sad_pack_seg s[16];
+  int n;
+};
+template <typename T>
+__global__ void adamw_pack_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                  float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
+                                  float bc1, float bc2_sqrt, PackSegs segs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float gi = g[i];
+  float pi = p[i] * (1.f - lr * wd);
+  const float mi = m[i] + (gi - m[i]) * (1.f - b1);
+  const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  pi -= (lr / bc1) * (mi / denom);
+  p[i] = pi;
+  m[i] = mi;
+  v[i] = vi;
+  for (int k = 0; k < segs.n; ++k) {
+    const sad_pack_seg& sg = segs.s[k];
+    const int kk = sg.k * sg.k;
+    const int64_t loc = i - sg.offset;
+    if (loc < 0 || loc >= (int64_t)sg.cout * sg.cin * kk) continue;
+    const int t = (int)(loc % kk), ci = (int)((loc / kk) % sg.cin), co = (int)(loc / ((int64_t)kk * sg.cin));
+    if (sg.mode0) st1((T*)sg.mode0 + ((int64_t)co * kk + t) * sg.cin + ci, pi);
+    if (sg.mode1) st1((T*)sg.mode1 + ((int64_t)ci * kk + (kk - 1 - t)) * sg.cout + co, pi);
+  }
+}
+
+extern "C" int sad_adamw_pack_run(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                                  float beta2, float eps, float weight_decay, int64_t step, const sad_pack_seg* segs,
+                                  int32_t nseg, int32_t dtype, void* stream) {
+  SAD_REQUIRE(p && g && m && v && n >= 0 && step >= 1, "bad args");
+  SAD_REQUIRE(nseg >= 0 && nseg <= 16 && (nseg == 0 || segs), "at most 16 pack segments");
+  SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
+  PackSegs ps{};
+  ps.n = nseg;
+  for (int k = 0; k < nseg; ++k) {
+    ps.s[k] = segs[k];
+    SAD_REQUIRE(segs[k].offset >= 0 && segs[k].cout > 0 && segs[k].cin > 0 && segs[k].k > 0 &&
+                    segs[k].offset + (int64_t)segs[k].cout * segs[k].cin * segs[k].k * segs[k].k <= n,
+                "pack segment outside the parameter range");
+  }
+  if (!n) return SAD_OK;
+  const float bc1 = (float)(1.0 - pow((double)beta1, (double)step));
+  const float bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
+  if (dtype == SAD_BF16)
+    hipLaunchKernelGGL(adamw_pack_kernel<u16>, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr,
+                       beta1, beta2, eps, weight_decay, bc1, bc2s, ps);
+  else
+    hipLaunchKernelGGL(adamw_pack_kernel<float>, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr,
+                       beta1, beta2, eps, weight_decay, bc1, bc2s, ps);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
 }
 
 extern "C" int sad_adamw_run(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,

@@ -37,6 +37,12 @@ class FrontendCfg(ctypes.Structure):
                 ('top_db', ctypes.c_float), ('n_samples', I32)]
 
 
+class PackSeg(ctypes.Structure):
+    """sad_pack_seg (include/sad.h)."""
+    _fields_ = [('offset', I64), ('cout', I32), ('cin', I32), ('k', I32), ('reserved', I32),
+                ('mode0', P), ('mode1', P)]
+
+
 SIGNATURES = {
     'sad_init': (ctypes.c_int, [ctypes.c_int]),
     'sad_last_error': (ctypes.c_char_p, []),
@@ -82,6 +88,9 @@ SIGNATURES = {
     'sad_stem_conv_run': (ctypes.c_int, [P, I64, I32, I32, P, P, SZ, P, I32, P]),
     'sad_stem_train_workspace_size': (ctypes.c_int, [I64, ctypes.POINTER(SZ)]),
     'sad_stem_train_run': (ctypes.c_int, [P, I64, P, P, P, ctypes.c_float, ctypes.c_float, P, P, P, P, P, SZ, P]),
+    'sad_conv_bn_train_workspace_size': (ctypes.c_int, [I64, I32, I32, I32, I32, I32, I32, ctypes.POINTER(SZ)]),
+    'sad_conv_bn_train_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, I32, I32, I32, I32, I32, P, P, ctypes.c_float,
+                                             ctypes.c_float, P, P, P, P, P, SZ, P, P]),
     'sad_bn_workspace_size': (ctypes.c_int, [I64, I32, ctypes.POINTER(SZ)]),
     'sad_bn_stats_run': (ctypes.c_int, [P, I64, I32, I32, P, P, ctypes.c_float, ctypes.c_float, P, P, P, P, SZ,
                                         P]),
@@ -99,6 +108,9 @@ SIGNATURES = {
     'sad_clip_grad_norm_run': (ctypes.c_int, [P, I64, ctypes.c_float, P, P, SZ, P]),
     'sad_adamw_run': (ctypes.c_int, [P, P, P, P, I64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                      ctypes.c_float, ctypes.c_float, I64, P]),
+    'sad_adamw_pack_run': (ctypes.c_int, [P, P, P, P, I64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_float, I64, ctypes.POINTER(PackSeg), I32, I32,
+                                          P]),
     'sad_axpy_run': (ctypes.c_int, [P, P, I64, ctypes.c_float, P]),
     'sad_avgpool_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, P]),
 }

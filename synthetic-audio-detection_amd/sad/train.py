@@ -252,9 +252,27 @@ class TrainNet:
             self._packed[key] = t
         return t
 
-    def invalidate(self, prefix: str):
-        for key in [k for k in self._packed if k[0].startswith(prefix)]:
+    def invalidate(self, prefix: str, keep_modes=()):
+        for key in [k for k in self._packed if k[0].startswith(prefix) and k[1] not in keep_modes]:
             del self._packed[key]
+
+    def pack_segments(self, prefix: str, base: int):
+        """sad_pack_seg entries for the conv weights under ``prefix`` whose
+        pack-mode 0 / 1 copies are cached (offsets relative to flat index
+        ``base``), for sad_adamw_pack_run."""
+        segs = []
+        for name in self.names:
+            if not (name.startswith(prefix) and name.endswith('.weight')):
+                continue
+            conv = name[:-len('.weight')]
+            m0, m1 = self._packed.get((conv, 0)), self._packed.get((conv, 1))
+            w = self.params[name]
+            if w.dim() != 4 or (m0 is None and m1 is None):
+                continue
+            co, ci, k, _ = w.shape
+            segs.append(_lib.PackSeg(self.offsets[name][0] - base, co, ci, k, 0, _lib.ptr(m0), _lib.ptr(m1)))
+        assert len(segs) <= 16
+        return segs
 
     def _bn_stats(self, x: torch.Tensor, key: str) -> torch.Tensor:
         C = x.shape[-1]
@@ -271,6 +289,26 @@ class TrainNet:
         if self.update_running:
             self.nbt[key] += 1
         return st
+
+    def _conv_bn(self, x, w, cout, k, stride, pad, key):
+        """raw conv (pack-mode-0 weights) + its train-mode BN statistics in one
+        call (bf16: summed in the conv epilogue)."""
+        N, H, W, Cin = x.shape
+        Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+        out = torch.empty(N, Ho, Wo, cout, device=self.device, dtype=self.tdtype)
+        st = torch.empty(4 * cout, device=self.device, dtype=torch.float32)
+        sz = _lib.SZ()
+        _lib.call('sad_conv_bn_train_workspace_size', N, H, W, cout, k, stride, pad, _lib.ctypes.byref(sz))
+        ws = self._buf('convbn', sz.value)
+        rm, rv = self.running[key] if self.update_running else (None, None)
+        with torch.cuda.device(self.device):
+            _lib.call('sad_conv_bn_train_run', _lib.ptr(x), N, H, W, Cin, _lib.ptr(w), cout, k, stride, pad, self._dt,
+                      _lib.ptr(self.params[f'{key}.weight']), _lib.ptr(self.params[f'{key}.bias']), BN_EPS,
+                      BN_MOMENTUM, _lib.ptr(rm), _lib.ptr(rv), _lib.ptr(st), _lib.ptr(out), _lib.ptr(ws), ws.numel(),
+                      None, self._stream())
+        if self.update_running:
+            self.nbt[key] += 1
+        return out, st
 
     def _bn_apply(self, x, st, res=None, rst=None, relu=True):
         C = x.shape[-1]
@@ -373,15 +411,13 @@ class TrainNet:
             del raw
         saved = {}
         for prefix, cin, cout, stride, has_ds in self.blocks:
-            c1 = self._conv(a, self.packed(f'{prefix}.conv1', 0), cout, 3, stride, 1)
-            st1 = self._bn_stats(c1, f'{prefix}.bn1')
+            c1, st1 = self._conv_bn(a, self.packed(f'{prefix}.conv1', 0), cout, 3, stride, 1, f'{prefix}.bn1')
             a1 = self._bn_apply(c1, st1, relu=True)
-            c2 = self._conv(a1, self.packed(f'{prefix}.conv2', 0), cout, 3, 1, 1)
-            st2 = self._bn_stats(c2, f'{prefix}.bn2')
+            c2, st2 = self._conv_bn(a1, self.packed(f'{prefix}.conv2', 0), cout, 3, 1, 1, f'{prefix}.bn2')
             cd = std = None
             if has_ds:
-                cd = self._conv(a, self.packed(f'{prefix}.downsample.0', 0), cout, 1, stride, 0)
-                std = self._bn_stats(cd, f'{prefix}.downsample.1')
+                cd, std = self._conv_bn(a, self.packed(f'{prefix}.downsample.0', 0), cout, 1, stride, 0,
+                                        f'{prefix}.downsample.1')
                 out = self._bn_apply(c2, st2, res=cd, rst=std, relu=True)
             else:
                 out = self._bn_apply(c2, st2, res=a, relu=True)
@@ -576,11 +612,15 @@ class Trainer:
         self.last_norm = net.clip_grad_norm(lo, b4)
         self.step_count += 1
         lr = self.current_lr
+        # AdamW, writing the updated layer4 conv weights straight into their cached
+        # pack-mode 0 / 1 copies; other cached layouts of layer4 are dropped
+        segs = net.pack_segments('layer4.', a4)
+        arr = (_lib.PackSeg * max(1, len(segs)))(*segs)
         with torch.cuda.device(self.device):
-            _lib.call('sad_adamw_run', _lib.ptr(net.pflat[a4:b4]), _lib.ptr(net.gflat[a4:b4]), _lib.ptr(self.m),
+            _lib.call('sad_adamw_pack_run', _lib.ptr(net.pflat[a4:b4]), _lib.ptr(net.gflat[a4:b4]), _lib.ptr(self.m),
                       _lib.ptr(self.v), b4 - a4, lr, ADAM_BETAS[0], ADAM_BETAS[1], ADAM_EPS, WEIGHT_DECAY,
-                      self.step_count, _lib.stream_handle(self.device))
-        net.invalidate('layer4.')
+                      self.step_count, arr, len(segs), net._dt, _lib.stream_handle(self.device))
+        net.invalidate('layer4.', keep_modes=(0, 1))
         return loss, int(correct), int(global_batch), True
 
     # ------------------------------------------------------------ checkpoints

@@ -87,8 +87,9 @@ def test_image_path_equals_map_path(merged_path, golden_frontend):
     a = model(img)
     b = model.forward_maps(torch.from_numpy(golden_frontend['std_map'][1:2]))
     assert (a - b).abs().max().item() <= 5e-4
-    with pytest.raises(NotImplementedError):
-        model(torch.randn(1, 3, 512, 512))
+    # distinct channels run the 3-channel stem (parity: test_gpu_img3.py)
+    c = model(torch.randn(1, 3, 512, 512))
+    assert c.shape == a.shape and torch.isfinite(c).all()
 
 
 @pytest.mark.parametrize('N,H,Cin,Cout,k,s,p,res', [

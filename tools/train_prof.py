@@ -14,7 +14,7 @@ def main():
     ap.add_argument('--top', type=int, default=40)
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r['Start_Timestamp']))
-    ends = [i for i, r in enumerate(rows) if r['Kernel_Name'].startswith('sad::adamw_kernel')]
+    ends = [i for i, r in enumerate(rows) if 'adamw' in r['Kernel_Name']]
     steps = list(zip(ends[a.skip:-1], ends[a.skip + 1:]))
     agg = collections.defaultdict(lambda: [0.0, 0])
     wall = 0.0
