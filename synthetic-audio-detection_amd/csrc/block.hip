@@ -650,6 +650,7 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
 
 int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s, bool x3 = false);
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s);
+int launch_halo_rw_x3(const BlockConvArgs& a, hipStream_t s);
 
 // halo kernel (variant 20): bf16 stride-1 3x3 with Cout <= 128 (layer1, layer2's
 // second block), where the implicit GEMM is L2->LDS-fill bound (convbench,
@@ -682,6 +683,14 @@ static int c128_variant() {
   }();
   return v;
 }
+// SAD_X3_RW=0 runs split-bf16 layer1 on the weight-ring halo kernel (variant 20) instead of variant 26 (A/B)
+static bool x3_rw() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_X3_RW");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
 static int block_device_cus() {
   static int cus[64] = {};
   int dev = 0;
@@ -696,7 +705,11 @@ static int block_device_cus() {
 int default_block_variant(const BlockConvArgs& a, int dtype) {
   // split-bf16: the halo kernel for the stride-1 convs of layer1 (Cout 64) and
   // layer2 (Cout 128), whose implicit GEMM is L2->LDS-fill bound
-  if (dtype == SAD_BF16X3) return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
+  if (dtype == SAD_BF16X3) {
+    // layer1 (64 -> 64): the resident-weight split-bf16 kernel (half the channels per workgroup)
+    if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64 && x3_rw()) return 26;
+    return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
+  }
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
   if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo()))) return 20;
   // small maps (the trainer's 64-segment layer4: M = 16384): 256x256 tiles would
@@ -720,6 +733,7 @@ bool block_conv_can_pool(const BlockConvArgs& a, int dtype) {
   return bp > 0 && a.Ho * a.Wo == bp && !a.res && a.M % bp == 0;
 }
 static bool variant_fits(int v, int cout) {
+  if (v == 26) return cout == 64;
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128};
   if (v == 20 || v == 21) return cout % 64 == 0;
   if (v == 25) return cout == 64;
@@ -787,6 +801,10 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   if (a.M == 0) return SAD_OK;
   const int v = variant > 0 ? variant : default_block_variant(a_in, dtype);
   SAD_REQUIRE(variant_fits(v, a.Cout), "variant's channel tile does not divide Cout");
+  if (dtype == SAD_BF16X3 && v == 26) {
+    SAD_REQUIRE(halo_ok(a_in, dtype), "split-bf16 halo conv: 3x3/s1/p1, H, W % 16");
+    return launch_halo_rw_x3(a, s);
+  }
   if (dtype == SAD_BF16X3 && (v == 20 || v == 21)) {
     SAD_REQUIRE(v == 20 && halo_ok(a_in, dtype), "split-bf16 halo conv: variant 20, 3x3/s1/p1, H, W % 16");
     return launch_halo_v(a, v, s, true);

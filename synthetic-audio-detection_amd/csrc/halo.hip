@@ -739,6 +739,264 @@ int launch_halo_rw(const BlockConvArgs& a, hipStream_t s) {
   return a.relu ? launch_halo_rw_t<false, true>(a, s) : launch_halo_rw_t<false, false>(a, s);
 }
 
+// ---------------------------------------------------------------------------
+// Split-bf16 (X3) resident-weight layer1 conv (variant 26): logical Cin = Cout
+// = 64, i.e. 128 bf16 input channels ([hi 32 | lo 32] x 2 chunks).
+//
+// The hi/lo weights of all 64 output channels (144 KB) do not fit beside the
+// patches, so a workgroup owns HALF the output channels (32: 72 KB resident,
+// [tap][chunk][32 co][128 B]) and the two halves of a 16x16 tile run as
+// neighbouring workgroups (one XCD: the second patch read hits L2).  The patch
+// has two 64-bf16-channel chunks, one LDS buffer each (2 x 41 KB), ping-ponged:
+// while chunk 0 of tile t is computed, chunk 1 of t is DMA'd; while chunk 1
+// is computed, chunk 0 of tile t+1 -- every DMA has 9 taps of cover, and a
+// tile needs two barriers (vs one per tap on the weight-ring kernel 20).
+// Each tap: W_hi.X_hi + W_lo.X_hi + W_hi.X_lo (12 MFMAs per wave); the
+// next tap's fragments are read between this tap's MFMAs.  8 waves, each 32
+// channels x 2 tile rows; the epilogue adds bias [+ residual hi + lo] and
+// stores hi/lo from registers.
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(512, 1) void halo_rw_x3_kernel(BlockConvArgs a) {
+  constexpr int NW = 8, TC = 2, TP = 2, TW = 16, TH = 16;
+  constexpr int PW = TW + 2, PR = PW * (TH + 2);  // 18 x 18 patch rows
+  constexpr int NDP = (PR + 7) / 8;               // 41 DMA pieces per chunk
+  constexpr int QP = (NDP + NW - 1) / NW;         // <= 6 per wave
+  constexpr int WBLK = 32 * 128;                  // one (tap, chunk) weight block
+  constexpr int WBYTES = 18 * WBLK;               // resident weights
+  constexpr int PATCH = NDP * 1024;
+  constexpr int BAD = 0x7FFFFFF0;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wp = wave;  // tile rows 2wp, 2wp+1; the workgroup's 32 channels
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int half = w & 1, grp = w >> 1, ngrp = gridDim.x >> 1;
+  const int tiles_x = a.W / TW, tiles_img = tiles_x * (a.H / TH);
+  const int tiles_p = a.N * tiles_img;
+  const int tp_begin = (int)((int64_t)grp * tiles_p / ngrp), tp_end = (int)((int64_t)(grp + 1) * tiles_p / ngrp);
+  if (tp_begin >= tp_end) return;
+
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, (int)a.wt_bytes, 0x00020000);
+  const int ps0 = (int)a.in0_pstride * 2;
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+  // patch pieces of tile pt (chunk offset added at issue; padding stays past num_records)
+  auto prep_patch = [&](int pt, int (&po)[QP]) __attribute__((always_inline)) {
+    const int b = pt / tiles_img, rem = pt - b * tiles_img;
+    const int oy0 = (rem / tiles_x) * TH, ox0 = (rem % tiles_x) * TW;
+#pragma unroll
+    for (int k = 0; k < QP; ++k) {
+      const int pr = 8 * (wave + NW * k) + (lane >> 3);
+      const int py = pr / PW, px = pr - py * PW;
+      const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+      po[k] = (pr < PR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+                  ? ((b * a.H + iy) * a.W + ix) * ps0 + ((lane & 7) ^ (pr & 6)) * 16
+                  : BAD;
+    }
+  };
+  auto patch_piece = [&](const int (&po)[QP], int k, int ch) __attribute__((always_inline)) {
+    if (NDP % NW == 0 || wave + NW * k < NDP)
+      dma16_m0(r0, po[k] == BAD ? BAD : po[k] + ch * 128, lds0 + WBYTES + ch * PATCH + (wave + NW * k) * 1024);
+  };
+
+  // ---- prologue: this half's weights (72 pieces, 9 per wave) + chunk 0 of the first tile
+  const int wrow = (int)a.wt_ld * 2;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int q = wave + NW * i;  // block q / 4 = tap * 2 + chunk, rows 8 (q % 4) + lane / 8
+    const int blk = q >> 2, col = 8 * (q & 3) + (lane >> 3);
+    dma16_m0(rw, (32 * half + col) * wrow + blk * 128 + ((lane & 7) ^ (col & 6)) * 16,
+             lds0 + blk * WBLK + (q & 3) * 1024);
+  }
+  int pcur[QP], pnext[QP];
+  prep_patch(tp_begin, pcur);
+#pragma unroll
+  for (int k = 0; k < QP; ++k) patch_piece(pcur, k, 0);
+
+  const int fr = lane & 15, fg = lane >> 4;
+  float bias[TC][4];
+#pragma unroll
+  for (int i = 0; i < TC; ++i) {
+    const float4 b4 = *(const float4*)(a.bias + 32 * half + i * 16 + fg * 4);
+    bias[i][0] = b4.x;
+    bias[i][1] = b4.y;
+    bias[i][2] = b4.z;
+    bias[i][3] = b4.w;
+  }
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint2 resv[TC][TP][2];
+
+  auto pix_index = [&](int t, int j) __attribute__((always_inline)) {
+    const int b = t / tiles_img, rem = t - b * tiles_img;
+    const int oy = (rem / tiles_x) * TH + 2 * wp + j, ox = (rem % tiles_x) * TW + fr;
+    return (int64_t)(b * a.Ho + oy) * a.Wo + ox;
+  };
+  // logical channel 32*half + i*16 + fg*4 (+0..3) -> split column 64*half + i*16 + fg*4 (hi), +32 (lo)
+  const int pc0 = 64 * half + fg * 4;
+  auto load_res = [&](int t, int j) __attribute__((always_inline)) {
+    if constexpr (RES) {
+      const u16* rp = (const u16*)a.res + pix_index(t, j) * a.res_pstride + pc0;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        resv[i][j][0] = *(const uint2*)(rp + i * 16);
+        resv[i][j][1] = *(const uint2*)(rp + i * 16 + 32);
+      }
+    }
+  };
+  auto epilogue = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      u16* op = (u16*)a.out + pix_index(t, j) * a.out_pstride + pc0;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[i][r];
+        if constexpr (RES) {
+          const uint2 h = resv[i][j][0], l = resv[i][j][1];
+          v[0] += __uint_as_float(h.x << 16) + __uint_as_float(l.x << 16);
+          v[1] += __uint_as_float(h.x & 0xFFFF0000u) + __uint_as_float(l.x & 0xFFFF0000u);
+          v[2] += __uint_as_float(h.y << 16) + __uint_as_float(l.y << 16);
+          v[3] += __uint_as_float(h.y & 0xFFFF0000u) + __uint_as_float(l.y & 0xFFFF0000u);
+        }
+        if constexpr (RELU)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        u16 hh[4], ll[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          hh[r] = f2bf(v[r]);
+          ll[r] = f2bf(v[r] - bf2f(hh[r]));
+        }
+        *(uint2*)(op + i * 16) =
+            make_uint2((uint32_t)hh[0] | ((uint32_t)hh[1] << 16), (uint32_t)hh[2] | ((uint32_t)hh[3] << 16));
+        *(uint2*)(op + i * 16 + 32) =
+            make_uint2((uint32_t)ll[0] | ((uint32_t)ll[1] << 16), (uint32_t)ll[2] | ((uint32_t)ll[3] << 16));
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  // fragments of (tap k, chunk ch): weights [half s][i], pixels [half s][j]; s = 0 hi, 1 lo
+  auto read_tap = [&](uint4 (&wf)[2][TC], uint4 (&pf)[2][TP], int k, int ch) __attribute__((always_inline)) {
+    const char* wb = smem + (k * 2 + ch) * WBLK;
+    const char* pbuf = smem + WBYTES + ch * PATCH;
+    const int ky = k / 3, kx = k - ky * 3;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = fg + 4 * s;
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const int r = i * 16 + fr;
+        wf[s][i] = *(const uint4*)(wb + r * 128 + (hswz(r, c) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int r = (2 * wp + j + ky) * PW + kx + fr;
+        pf[s][j] = *(const uint4*)(pbuf + r * 128 + (hswz(r, c) << 4));
+      }
+    }
+  };
+  auto mma_tap = [&](const uint4 (&wf)[2][TC], const uint4 (&pf)[2][TP]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < TC; ++i)
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        mfma_chunk<u16>(wf[0][i], pf[0][j], acc[i][j]);  // W_hi . X_hi
+        mfma_chunk<u16>(wf[1][i], pf[0][j], acc[i][j]);  // W_lo . X_hi
+        mfma_chunk<u16>(wf[0][i], pf[1][j], acc[i][j]);  // W_hi . X_lo
+      }
+  };
+  // 9 taps of chunk ch; during taps k < QP the wave issues piece k of `issue`
+  // (chunk ich of the pieces in po) -- the other chunk buffer is free
+  uint4 wf[2][2][TC], pf[2][2][TP];
+  auto chunk = [&](int ch, bool issue, const int (&po)[QP], int ich, int res_t) __attribute__((always_inline)) {
+    read_tap(wf[0], pf[0], 0, ch);
+    static_for<9>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (k < QP)
+        if (issue) patch_piece(po, k, ich);
+      if constexpr (RES && k >= QP && k < QP + TP)
+        if (res_t >= 0) load_res(res_t, k - QP);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (k < 8) {
+        read_tap(wf[(k + 1) & 1], pf[(k + 1) & 1], k + 1, ch);
+        mma_tap(wf[k & 1], pf[k & 1]);
+#pragma unroll
+        for (int q = 0; q < 2 * (TC + TP); ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 3 * TC * TP - 2 * (TC + TP), 0);
+      } else {
+        mma_tap(wf[k & 1], pf[k & 1]);
+      }
+    });
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int t = tp_begin; t < tp_end; ++t) {
+    const bool has_next = t + 1 < tp_end;
+    // chunk 0 of t from buffer 0; chunk 1 of t goes into buffer 1
+    chunk(0, true, pcur, 1, -1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // chunk 1 published, buffer 0 free
+    if (has_next) prep_patch(t + 1, pnext);
+    // chunk 1 of t from buffer 1; chunk 0 of t+1 goes into buffer 0; residual of t
+    chunk(1, has_next, pnext, 0, t);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    epilogue(t);
+    __builtin_amdgcn_s_barrier();  // chunk 0 of t+1 published, buffer 1 free
+#pragma unroll
+    for (int k = 0; k < QP; ++k) pcur[k] = pnext[k];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool RES, bool RELU>
+static int launch_halo_rw_x3_t(const BlockConvArgs& a, hipStream_t s) {
+  constexpr int smem = 18 * 32 * 128 + 2 * 41 * 1024;
+  static_assert(smem <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)halo_rw_x3_kernel<RES, RELU>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              smem);
+    attr = true;
+  }
+  const int64_t tiles_p = (int64_t)a.N * (a.H / 16) * (a.W / 16);
+  const int64_t g = std::min<int64_t>(tiles_p, 128) * 2;
+  hipLaunchKernelGGL((halo_rw_x3_kernel<RES, RELU>), dim3((unsigned)g), dim3(512), smem, s, a);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
+}
+
+// (a: the split layout's bf16 channel counts / strides, as launch_block_conv passes them)
+int launch_halo_rw_x3(const BlockConvArgs& a, hipStream_t s) {
+  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.in1,
+              "halo conv: 3x3, stride 1, pad 1, no GEMM shortcut");
+  SAD_REQUIRE(a.Cin == 128 && a.Cout == 64, "split-bf16 resident-weight halo conv (variant 26): 64 -> 64 logical");
+  SAD_REQUIRE(a.W % 16 == 0 && a.H % 16 == 0 && a.Ho == a.H && a.Wo == a.W, "image must tile exactly");
+  SAD_REQUIRE(a.wt_ld >= 9 * a.Cin && (a.wt_ld * 2) % 16 == 0, "weight row length");
+  SAD_REQUIRE(a.out_pstride % 64 == 0 && (!a.res || a.res_pstride % 64 == 0), "split-bf16 pixel strides");
+  SAD_REQUIRE(!a.st_part, "fused BN statistics: not on the split-bf16 kernels");
+  const int64_t tiles_p = (int64_t)a.N * (a.H / 16) * (a.W / 16);
+  SAD_REQUIRE(tiles_p < (1ll << 30) && (int64_t)a.N * a.H * a.W * a.in0_pstride * 2 < (1ll << 31),
+              "too large for one launch");
+  if (a.res) return a.relu ? launch_halo_rw_x3_t<true, true>(a, s) : launch_halo_rw_x3_t<true, false>(a, s);
+  return a.relu ? launch_halo_rw_x3_t<false, true>(a, s) : launch_halo_rw_x3_t<false, false>(a, s);
+}
+
 template <int WC, int WP, int TC, int TP, int TW, bool RES, bool RELU, bool X3, bool ST = false>
 static int launch_halo_t(const BlockConvArgs& a, hipStream_t s) {
   using G = HaloGeo<WC, WP, TC, TP, TW, X3>;

@@ -79,10 +79,13 @@ def test_block_conv_x3_vs_float64(cin, cout, H, stride, shortcut, variant):
     assert err <= 1e-4, err
 
 
-@pytest.mark.parametrize('c,H,res', [(64, 32, True), (64, 48, False), (128, 16, True), (128, 32, False)])
-def test_halo_conv_x3_vs_float64(c, H, res):
-    """The split-bf16 halo kernel (variant 20: layer1 / layer2 stride-1 convs,
-    identity shortcut as an epilogue residual) vs float64."""
+@pytest.mark.parametrize('c,H,res,variant', [(64, 32, True, 20), (64, 48, False, 20), (128, 16, True, 20),
+                                             (128, 32, False, 20), (64, 32, True, 26), (64, 48, False, 26),
+                                             (64, 16, True, 26), (64, 80, True, 26)])
+def test_halo_conv_x3_vs_float64(c, H, res, variant):
+    """The split-bf16 halo kernels (variant 20: weight ring, layer2 stride-1
+    convs; variant 26: resident weights, half the channels per workgroup,
+    layer1) with the identity shortcut as an epilogue residual, vs float64."""
     from sad.engine import block_conv, from_split, to_split
     g = torch.Generator().manual_seed(c + H + int(res))
     N = 3
@@ -93,11 +96,11 @@ def test_halo_conv_x3_vs_float64(c, H, res):
     y = F.conv2d(x.permute(0, 3, 1, 2).double(), w.double(), bias.double(), padding=1).permute(0, 2, 3, 1)
     ref = (y + (r.double() if res else 0)).clamp_min(0)
     wk = w.permute(0, 2, 3, 1).reshape(c, 9 * c)
-    out = block_conv(to_split(x).to(DEV), to_split(wk).to(DEV), bias.to(DEV), variant=20, split=True,
+    out = block_conv(to_split(x).to(DEV), to_split(wk).to(DEV), bias.to(DEV), variant=variant, split=True,
                      res=to_split(r).to(DEV) if res else None)
     torch.cuda.synchronize()
     err = ((from_split(out.cpu()).double() - ref).abs().max() / ref.abs().max()).item()
-    print(f'x3 halo conv c{c} H{H} res={res}: rel err {err:.3e}')
+    print(f'x3 halo conv v{variant} c{c} H{H} res={res}: rel err {err:.3e}')
     assert err <= 1e-4, err
 
 
