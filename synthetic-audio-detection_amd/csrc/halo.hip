@@ -949,12 +949,17 @@ __global__ __launch_bounds__(512, 1) void halo_rw_x3_kernel(BlockConvArgs a) {
   for (int t = tp_begin; t < tp_end; ++t) {
     const bool has_next = t + 1 < tp_end;
     // chunk 0 of t from buffer 0; chunk 1 of t goes into buffer 1
-    chunk(0, true, pcur, 1, -1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (this tile's residual goes out at taps QP.. of chunk 0, the youngest loads:
+    // the wait below leaves them in flight, so they get chunk 1 as cover)
+    chunk(0, true, pcur, 1, t);
+    if constexpr (RES)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * TC * TP) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // chunk 1 published, buffer 0 free
     if (has_next) prep_patch(t + 1, pnext);
-    // chunk 1 of t from buffer 1; chunk 0 of t+1 goes into buffer 0; residual of t
-    chunk(1, has_next, pnext, 0, t);
+    // chunk 1 of t from buffer 1; chunk 0 of t+1 goes into buffer 0
+    chunk(1, has_next, pnext, 0, -1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     epilogue(t);
     __builtin_amdgcn_s_barrier();  // chunk 0 of t+1 published, buffer 1 free
