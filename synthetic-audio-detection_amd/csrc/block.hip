@@ -379,10 +379,11 @@ if constexpr (X3) {
 #pragma unroll
       for (int i = 0; i < TC; ++i)
 #pragma unroll
-        for (int j = 0; j < TP; ++j) {
-          mfma_chunk<T>(wf[1][i], pf[0][j], acc[i][j]);
-          mfma_chunk<T>(wf[0][i], pf[1][j], acc[i][j]);
-        }
+        for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[1][i], pf[0][j], acc[i][j]);
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[0][i], pf[1][j], acc[i][j]);
     } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)

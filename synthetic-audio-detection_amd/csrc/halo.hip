@@ -361,10 +361,11 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
 #pragma unroll
       for (int i = 0; i < TC; ++i)
 #pragma unroll
-        for (int j = 0; j < TP; ++j) {
-          mfma_chunk<u16>(w[1][i], p[0][j], acc[i][j]);
-          mfma_chunk<u16>(w[0][i], p[1][j], acc[i][j]);
-        }
+        for (int j = 0; j < TP; ++j) mfma_chunk<u16>(w[1][i], p[0][j], acc[i][j]);
+#pragma unroll
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j) mfma_chunk<u16>(w[0][i], p[1][j], acc[i][j]);
     } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -906,14 +907,15 @@ __global__ __launch_bounds__(512, 1) void halo_rw_x3_kernel(BlockConvArgs a) {
     }
   };
   auto mma_tap = [&](const uint4 (&wf)[2][TC], const uint4 (&pf)[2][TP]) __attribute__((always_inline)) {
+    // product-outer: a product's TC*TP MFMAs go to independent accumulators, so
+    // dependent MFMAs (same accumulator) are TC*TP issues apart, not back to back
 #pragma unroll
-    for (int i = 0; i < TC; ++i)
+    for (int p = 0; p < 3; ++p)
 #pragma unroll
-      for (int j = 0; j < TP; ++j) {
-        mfma_chunk<u16>(wf[0][i], pf[0][j], acc[i][j]);  // W_hi . X_hi
-        mfma_chunk<u16>(wf[1][i], pf[0][j], acc[i][j]);  // W_lo . X_hi
-        mfma_chunk<u16>(wf[0][i], pf[1][j], acc[i][j]);  // W_hi . X_lo
-      }
+      for (int i = 0; i < TC; ++i)
+#pragma unroll
+        for (int j = 0; j < TP; ++j)
+          mfma_chunk<u16>(wf[p == 1 ? 1 : 0][i], pf[p == 2 ? 1 : 0][j], acc[i][j]);  // hi.hi, lo.hi, hi.lo
   };
   // 9 taps of chunk ch; during taps k < QP the wave issues piece k of `issue`
   // (chunk ich of the pieces in po) -- the other chunk buffer is free
