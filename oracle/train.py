@@ -51,12 +51,13 @@ def segment_image(wave: torch.Tensor, mask=None, box=None) -> torch.Tensor:
 
 
 class TrainModel(nn.Module):
-    """timm resnet18 / resnet34 (num_classes=0) + the trainer's (unused) head."""
+    """timm resnet18/34/50/... (num_classes=0) + the trainer's (unused) head,
+    ``nn.Linear(model.num_features, 512)`` first (submodel_trainer.py:613-625)."""
 
     def __init__(self, model_name: str = 'resnet18'):
         super().__init__()
         self.base = ores.create_model(model_name, num_classes=0)
-        self.head = ores.make_head(512)
+        self.head = ores.make_head(2048 if model_name in ('resnet50', 'resnet101', 'resnet152') else 512)
 
     def forward(self, x):
         return self.base(x)  # timm forward: pooled features (head unused, quirk C1)

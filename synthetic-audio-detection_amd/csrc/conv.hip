@@ -659,11 +659,11 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
           al.y = *(const uint32_t*)(pl + 2);
           al.z = *(const uint32_t*)(pl + 4);
           al.w = *(const uint32_t*)(pl + 6);
+          // product-outer: 4 independent accumulators between dependent MFMAs
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            mfma_chunk<u16>(av, bwl[j][s], r[i][j]);  // X_hi . W_lo
-            mfma_chunk<u16>(al, bw[j][s], r[i][j]);   // X_lo . W_hi
-          }
+          for (int j = 0; j < 4; ++j) mfma_chunk<u16>(av, bwl[j][s], r[i][j]);  // X_hi . W_lo
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mfma_chunk<u16>(al, bw[j][s], r[i][j]);   // X_lo . W_hi
         }
       }
     }

@@ -39,7 +39,7 @@ import torch
 
 from . import _lib
 from .engine import MAP_H, MAP_W, Backbone, FrontEnd, ResNetBackbone, _dev
-from .weights import HEAD_LAYOUT, arch_param_shapes, arch_spec, backbone_param_shapes
+from .weights import HEAD_LAYOUT, arch_param_shapes, arch_spec, backbone_param_shapes, head_layout
 
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
@@ -66,11 +66,25 @@ def block_table(layers=(2, 2, 2, 2)):
 BLOCKS = block_table()
 
 
-def _basic_layers(model_name: str):
-    block, layers, _ = arch_spec(model_name)
-    if block != 'basic':
-        raise ValueError(f'the device trainer runs BasicBlock ResNets (resnet18/34), not {model_name!r}')
-    return layers
+def bottleneck_table(layers=(3, 4, 6, 3)):
+    """[(prefix, cin, cout, stride, has_downsample, width)] of a timm Bottleneck
+    ResNet (resnet50/101/152): width = planes, cout = 4 * planes, stride on conv2,
+    a downsample wherever the shape changes (incl. layer1.0: 64 -> 256)."""
+    out, inp = [], 64
+    for li, planes in enumerate((64, 128, 256, 512)):
+        for b in range(layers[li]):
+            s = 2 if (b == 0 and li > 0) else 1
+            out.append((f'layer{li + 1}.{b}', inp, 4 * planes, s, b == 0, planes))
+            inp = 4 * planes
+    return out
+
+
+def _blocks(model_name: str):
+    """(is_bottleneck, block table, num_features) of a supported timm ResNet."""
+    block, layers, nf = arch_spec(model_name)
+    if block == 'bottleneck':
+        return True, bottleneck_table(layers), nf
+    return False, block_table(layers), nf
 
 
 def param_layout(model_name: str = 'resnet18'):
@@ -111,10 +125,11 @@ def init_state_dict(seed: int = 42, model_name: str = 'resnet18'):
     convs = {k: torch.empty(s) for k, s, kind in layout if kind == 'conv'}
     # construction order: conv1, then per stage: downsample.0, block convs
     order = ['conv1']
-    for prefix, _, _, _, has_ds in block_table(_basic_layers(model_name)):
+    bottleneck, blocks, nf = _blocks(model_name)
+    for prefix, _, _, _, has_ds, *_ in blocks:
         if has_ds:
             order.append(f'{prefix}.downsample.0')
-        order += [f'{prefix}.conv1', f'{prefix}.conv2']
+        order += [f'{prefix}.conv1', f'{prefix}.conv2'] + ([f'{prefix}.conv3'] if bottleneck else [])
     for k in order:
         torch.nn.init.kaiming_uniform_(convs[k], a=math.sqrt(5), generator=g)
     sd = OrderedDict()
@@ -124,12 +139,13 @@ def init_state_dict(seed: int = 42, model_name: str = 'resnet18'):
             sd[f'{k}.weight'] = convs[k]
         else:
             c = s[0]
-            w = torch.zeros(c) if k.endswith('.bn2') else torch.ones(c)
+            last = '.bn3' if bottleneck else '.bn2'  # zero_init_last
+            w = torch.zeros(c) if k.endswith(last) else torch.ones(c)
             sd[f'{k}.weight'], sd[f'{k}.bias'] = w, torch.zeros(c)
             sd[f'{k}.running_mean'], sd[f'{k}.running_var'] = torch.zeros(c), torch.ones(c)
             sd[f'{k}.num_batches_tracked'] = torch.tensor(0, dtype=torch.long)
     hd = OrderedDict()
-    for idx, kind, shape in HEAD_LAYOUT:
+    for idx, kind, shape in head_layout(nf):
         if kind == 'linear':  # nn.Linear.reset_parameters
             w = torch.empty(shape)
             torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5), generator=g)
@@ -192,7 +208,7 @@ class TrainNet:
                  dtype: str = 'bf16', model_name: str = 'resnet18'):
         self.device = _dev(device)
         self.model_name = model_name
-        self.blocks = block_table(_basic_layers(model_name))
+        self.bottleneck, self.blocks, self.num_features = _blocks(model_name)
         self.dtype = dtype
         self._dt = _lib.SAD_BF16 if dtype == 'bf16' else _lib.SAD_F32
         self.tdtype = torch.bfloat16 if dtype == 'bf16' else torch.float32
@@ -220,7 +236,7 @@ class TrainNet:
         self.head_sd = OrderedDict((k, torch.as_tensor(head_sd[k]).detach().clone().cpu()) for k in head_keys())
         self.range4 = (self.offsets['layer4.0.conv1.weight'][0], total)
         self.range3 = (self.offsets['layer3.0.conv1.weight'][0], self.range4[0])
-        self.zero_bias = torch.zeros(FEATURES, device=self.device, dtype=torch.float32)
+        self.zero_bias = torch.zeros(max(FEATURES, self.num_features), device=self.device, dtype=torch.float32)
         self._packed = {}
         self._ws = {}
         self.update_running = True
@@ -410,7 +426,10 @@ class TrainNet:
                           _lib.ptr(a), s)
             del raw
         saved = {}
-        for prefix, cin, cout, stride, has_ds in self.blocks:
+        if self.bottleneck:
+            for blk in self.blocks:
+                a = self._bottleneck_fwd(a, blk, saved, keep_from)
+        for prefix, cin, cout, stride, has_ds in ([] if self.bottleneck else self.blocks):
             c1, st1 = self._conv_bn(a, self.packed(f'{prefix}.conv1', 0), cout, 3, stride, 1, f'{prefix}.bn1')
             a1 = self._bn_apply(c1, st1, relu=True)
             c2, st2 = self._conv_bn(a1, self.packed(f'{prefix}.conv2', 0), cout, 3, 1, 1, f'{prefix}.bn2')
@@ -424,9 +443,9 @@ class TrainNet:
             if int(prefix[5]) >= keep_from:
                 saved[prefix] = dict(x=a, c1=c1, st1=st1, a1=a1, c2=c2, st2=st2, cd=cd, std=std, out=out)
             a = out
-        feats = torch.empty(B, FEATURES, device=self.device, dtype=torch.float32)
+        feats = torch.empty(B, self.num_features, device=self.device, dtype=torch.float32)
         with torch.cuda.device(self.device):
-            _lib.call('sad_avgpool_run', _lib.ptr(a), B, a.shape[1] * a.shape[2], FEATURES, self._dt,
+            _lib.call('sad_avgpool_run', _lib.ptr(a), B, a.shape[1] * a.shape[2], self.num_features, self._dt,
                       _lib.ptr(feats), s)
         return feats, saved
 
@@ -437,6 +456,9 @@ class TrainNet:
         3 in layers) into ``grads3`` (overwritten; the caller folds them into the
         accumulating .grad, quirk C4)."""
         order = [b for b in reversed(self.blocks) if int(b[0][5]) in layers]
+        if self.bottleneck:
+            self._bottleneck_bwd(dfeat, saved, order, grads3)
+            return
         dy, dpool = None, dfeat
         for bi, (prefix, cin, cout, stride, has_ds) in enumerate(order):
             sv = saved[prefix]
@@ -459,6 +481,64 @@ class TrainNet:
             else:
                 dx = torch.empty_like(sv['x'])
                 self._dgrad_gemm(dc1, f'{prefix}.conv1', sv['x'].shape, 3, stride, 1, dx, False)
+                self._dgrad_gemm(dcd, f'{prefix}.downsample.0', sv['x'].shape, 1, stride, 0, dx, True)
+            dy, dpool = dx, None
+
+    # ---------------------------------------------------------- Bottleneck
+    def _bottleneck_fwd(self, x, blk, saved, keep_from):
+        """timm Bottleneck in train mode: 1x1 -> bn1/ReLU -> 3x3/s -> bn2/ReLU ->
+        1x1 -> bn3 (+ downsample 1x1/s + BN, or identity) -> ReLU."""
+        prefix, cin, cout, stride, has_ds, width = blk
+        c1, st1 = self._conv_bn(x, self.packed(f'{prefix}.conv1', 0), width, 1, 1, 0, f'{prefix}.bn1')
+        a1 = self._bn_apply(c1, st1, relu=True)
+        c2, st2 = self._conv_bn(a1, self.packed(f'{prefix}.conv2', 0), width, 3, stride, 1, f'{prefix}.bn2')
+        a2 = self._bn_apply(c2, st2, relu=True)
+        c3, st3 = self._conv_bn(a2, self.packed(f'{prefix}.conv3', 0), cout, 1, 1, 0, f'{prefix}.bn3')
+        cd = std = None
+        if has_ds:
+            cd, std = self._conv_bn(x, self.packed(f'{prefix}.downsample.0', 0), cout, 1, stride, 0,
+                                    f'{prefix}.downsample.1')
+            out = self._bn_apply(c3, st3, res=cd, rst=std, relu=True)
+        else:
+            out = self._bn_apply(c3, st3, res=x, relu=True)
+        if int(prefix[5]) >= keep_from:
+            saved[prefix] = dict(x=x, c1=c1, st1=st1, a1=a1, c2=c2, st2=st2, a2=a2, c3=c3, st3=st3, cd=cd, std=std,
+                                 out=out)
+        return out
+
+    def _bottleneck_bwd(self, dfeat, saved, order, grads3):
+        dy, dpool = None, dfeat
+        for bi, (prefix, cin, cout, stride, has_ds, width) in enumerate(order):
+            sv = saved[prefix]
+            G = self.grads if prefix.startswith('layer4') else grads3
+            Ho = sv['c3'].shape[1]
+            dc3, dz3 = self._bn_backward(sv['c3'], sv['st3'], f'{prefix}.bn3', G, dy=dy, dpool=dpool,
+                                         pool_hw=Ho * Ho if dpool is not None else 0, y=sv['out'], want_dz=True)
+            dcd = None
+            if has_ds:
+                dcd, _ = self._bn_backward(sv['cd'], sv['std'], f'{prefix}.downsample.1', G, dy=dz3)
+                self._wgrad(sv['x'], dcd, f'{prefix}.downsample.0', G, 1, stride, 0)
+            self._wgrad(sv['a2'], dc3, f'{prefix}.conv3', G, 1, 1, 0)
+            da2 = self._conv(dc3, self.packed(f'{prefix}.conv3', 1), width, 1, 1, 0)
+            dc2, _ = self._bn_backward(sv['c2'], sv['st2'], f'{prefix}.bn2', G, dy=da2, y=sv['a2'])
+            self._wgrad(sv['a1'], dc2, f'{prefix}.conv2', G, 3, stride, 1)
+            if stride == 1:
+                da1 = self._conv(dc2, self.packed(f'{prefix}.conv2', 1), width, 3, 1, 1)
+            else:
+                da1 = torch.empty_like(sv['a1'])
+                self._dgrad_gemm(dc2, f'{prefix}.conv2', sv['a1'].shape, 3, stride, 1, da1, False)
+            dc1, _ = self._bn_backward(sv['c1'], sv['st1'], f'{prefix}.bn1', G, dy=da1, y=sv['a1'])
+            self._wgrad(sv['x'], dc1, f'{prefix}.conv1', G, 1, 1, 0)
+            if bi + 1 == len(order):
+                break
+            # dx = conv1's dgrad (1x1, stride 1) + the shortcut's gradient
+            if not has_ds:
+                dx = self._conv(dc1, self.packed(f'{prefix}.conv1', 1), cin, 1, 1, 0, res=dz3)
+            elif stride == 1:
+                dx = self._conv(dc1, self.packed(f'{prefix}.conv1', 1), cin, 1, 1, 0)
+                self._dgrad_gemm(dcd, f'{prefix}.downsample.0', sv['x'].shape, 1, 1, 0, dx, True)
+            else:
+                dx = self._conv(dc1, self.packed(f'{prefix}.conv1', 1), cin, 1, 1, 0)
                 self._dgrad_gemm(dcd, f'{prefix}.downsample.0', sv['x'].shape, 1, stride, 0, dx, True)
             dy, dpool = dx, None
 

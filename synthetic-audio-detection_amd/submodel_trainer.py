@@ -455,9 +455,6 @@ def main(argv=None):
         logging.error(f"Requested number of GPUs ({args.num_gpus}) is greater than available GPUs "
                       f"({torch.cuda.device_count()})")
         sys.exit(1)
-    if args.model_name not in ('resnet18', 'resnet34'):
-        raise NotImplementedError(f'--model-name {args.model_name}: the MI355X trainer kernels implement the '
-                                  'BasicBlock ResNets (resnet18, resnet34)')
     if not torch.cuda.is_available():
         raise RuntimeError('submodel_trainer runs on MI355X GPUs only (no CPU path)')
     torch.cuda.set_device(local)

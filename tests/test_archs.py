@@ -51,7 +51,24 @@ def test_trainer_tables_resnet34():
     assert list(base) == list(sw.backbone_state_dict(0, 'resnet34'))
     assert all((base[f'{b[0]}.bn2.weight'] == 0).all() for b in blocks)  # timm zero_init_last
     with pytest.raises(ValueError):
-        st.init_state_dict(42, 'resnet50')
+        st.init_state_dict(42, 'resnet26')
+
+
+def test_trainer_tables_resnet50():
+    """Bottleneck training tables: timm's key order, width / expansion, the
+    downsample on every stage's first block (layer1.0 too: 64 -> 256), stride on
+    conv2, zero_init_last on bn3, and the 2048-wide head input."""
+    from sad import train as st
+    blocks = st.bottleneck_table(sw.ARCHS['resnet50'][1])
+    assert len(blocks) == 16 and [b[0] for b in blocks][:4] == ['layer1.0', 'layer1.1', 'layer1.2', 'layer2.0']
+    assert blocks[0][1:] == (64, 256, 1, True, 64) and blocks[3][1:] == (256, 512, 2, True, 128)
+    assert blocks[-1][1:] == (2048, 2048, 1, False, 512)
+    base, head = st.init_state_dict(42, 'resnet50')
+    assert list(base) == list(sw.backbone_state_dict(0, 'resnet50'))
+    assert all((base[f'{b[0]}.bn3.weight'] == 0).all() for b in blocks)
+    assert all((base[f'{b[0]}.bn2.weight'] == 1).all() for b in blocks)
+    assert head['2.weight'].shape == (512, 2048)
+    assert [n for n, _ in st.param_layout('resnet50')][-2:] == ['layer4.2.bn3.weight', 'layer4.2.bn3.bias']
 
 
 def test_bench_arch_flop_counts():
