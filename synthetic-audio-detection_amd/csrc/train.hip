@@ -135,39 +135,49 @@ __device__ __forceinline__ void bl_axis(int o, int in, int on, int& i0, int& i1,
 // back to out x out (:466), composed exactly: each output pixel interpolates 4
 // crop pixels, each of which interpolates 4 map pixels.  The reference's 3
 // identical channels (:203) are one plane here.
+// One workgroup per output row: the row's two crop rows (bi + cy0, bi + cy1)
+// are evaluated once over the box's columns into LDS (each 512-image pixel =
+// 4 map gathers), then every output pixel is one 2x2 lerp from LDS -- half the
+// gathers of the per-pixel form and no repeated bl_axis work.
 template <typename OT>
-__global__ void crop_resize_kernel(const float* __restrict__ map, int mh, int mw, const int* __restrict__ boxes,
-                                   int out_hw, OT* __restrict__ img, int64_t total) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= total) return;
-  const int ox = (int)(idx % out_hw);
-  const int oy = (int)((idx / out_hw) % out_hw);
-  const int64_t n = idx / ((int64_t)out_hw * out_hw);
+__global__ __launch_bounds__(256) void crop_resize_kernel(const float* __restrict__ map, int mh, int mw,
+                                                          const int* __restrict__ boxes, int out_hw,
+                                                          OT* __restrict__ img) {
   constexpr int R = 512;  // the reference's Resize((512,512))
+  __shared__ float rows[2][R];
+  const int oy = blockIdx.x;
+  const int64_t n = blockIdx.y;
   int bi = 0, bj = 0, bh = R, bw = R;
   if (boxes) {
     bi = boxes[n * 4 + 0];
     bj = boxes[n * 4 + 1];
     bh = boxes[n * 4 + 2];
-    bw = boxes[n * 4 + 3];
+    bw = min(boxes[n * 4 + 3], R);  // a valid box lies inside the 512 x 512 image
   }
   const float* p = map + n * mh * mw;
-  int cy0, cy1, cx0, cx1;
-  float ly, lx;
+  int cy0, cy1;
+  float ly;
   bl_axis(oy, bh, out_hw, cy0, cy1, ly);
-  bl_axis(ox, bw, out_hw, cx0, cx1, lx);
-  auto img512 = [&](int iy, int ix) {
+  // crop columns [0, bw) of crop rows cy0, cy1 (bw <= 512)
+  for (int e = threadIdx.x; e < 2 * bw; e += blockDim.x) {
+    const int r = e >= bw, cx = e - r * bw;
+    const int iy = bi + (r ? cy1 : cy0), ix = bj + cx;
     int y0, y1, x0, x1;
     float a, b;
     bl_axis(iy, mh, R, y0, y1, a);
     bl_axis(ix, mw, R, x0, x1, b);
-    return (1.f - a) * ((1.f - b) * p[y0 * mw + x0] + b * p[y0 * mw + x1]) +
-           a * ((1.f - b) * p[y1 * mw + x0] + b * p[y1 * mw + x1]);
-  };
-  const float v00 = img512(bi + cy0, bj + cx0), v01 = img512(bi + cy0, bj + cx1);
-  const float v10 = img512(bi + cy1, bj + cx0), v11 = img512(bi + cy1, bj + cx1);
-  const float v = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
-  st1(img + idx, v);
+    rows[r][cx] = (1.f - a) * ((1.f - b) * p[y0 * mw + x0] + b * p[y0 * mw + x1]) +
+                  a * ((1.f - b) * p[y1 * mw + x0] + b * p[y1 * mw + x1]);
+  }
+  __syncthreads();
+  OT* o = img + ((int64_t)n * out_hw + oy) * out_hw;
+  for (int ox = threadIdx.x; ox < out_hw; ox += blockDim.x) {
+    int cx0, cx1;
+    float lx;
+    bl_axis(ox, bw, out_hw, cx0, cx1, lx);
+    const float v00 = rows[0][cx0], v01 = rows[0][cx1], v10 = rows[1][cx0], v11 = rows[1][cx1];
+    st1(o + ox, (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11));
+  }
 }
 
 // conv1 7x7/2/p3 of the one-plane image as im2col rows: col[p][k] for
@@ -696,14 +706,15 @@ extern "C" int sad_crop_resize_run(const float* map, int64_t n, int32_t h, int32
                                    int32_t out_hw, int32_t dtype, void* img, void* stream) {
   SAD_REQUIRE(map && img && n >= 0 && h > 0 && w > 0 && out_hw > 0, "bad args");
   SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16, "dtype");
-  const int64_t total = n * out_hw * out_hw;
-  if (!total) return SAD_OK;
+  SAD_REQUIRE(n <= 65535, "crop_resize: n > 65535");
+  if (!n) return SAD_OK;
+  const dim3 grid((unsigned)out_hw, (unsigned)n);
   if (dtype == SAD_BF16)
-    hipLaunchKernelGGL(crop_resize_kernel<u16>, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, map, h, w, boxes,
-                       out_hw, (u16*)img, total);
+    hipLaunchKernelGGL(crop_resize_kernel<u16>, grid, dim3(256), 0, (hipStream_t)stream, map, h, w, boxes, out_hw,
+                       (u16*)img);
   else
-    hipLaunchKernelGGL(crop_resize_kernel<float>, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, map, h, w,
-                       boxes, out_hw, (float*)img, total);
+    hipLaunchKernelGGL(crop_resize_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, map, h, w, boxes, out_hw,
+                       (float*)img);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }

@@ -346,22 +346,31 @@ __global__ __launch_bounds__(WM * WN * 64) void kouter_bf16_kernel(KoArgs g) {
   }
 }
 
-// dW[co][ci0 .. ci0+63][tap] = beta*dW + sum_s part[s][tap][co][ci] (fixed
-// order: deterministic).  Block = one co x 64 ci: partial rows are read
-// coalesced per tap, transposed through LDS, and written as one contiguous
-// 64*taps-float run of the OIHW gradient.
+// dW[co][ci0 .. ci0+255][tap] = beta*dW + sum_s part[s][tap][co][ci] (fixed
+// order: deterministic).  Block = one co x 256 ci: partial rows are read as
+// float4 per tap, transposed through LDS, and written as one contiguous
+// 256*taps-float run of the OIHW gradient.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int taps,
                                                            int M, int N, float beta, float* __restrict__ dw) {
-  __shared__ float sm[64 * 9 + 64];
-  const int co = blockIdx.y, ci0 = blockIdx.x * 64;
-  const int ci = threadIdx.x & 63, tg = threadIdx.x >> 6;
+  __shared__ float sm[256 * 9];
+  const int co = blockIdx.y, ci0 = blockIdx.x * 256;
+  const int c4 = threadIdx.x & 63, tg = threadIdx.x >> 6;
   const int64_t plane = (int64_t)M * N;
-  const int nci = min(64, N - ci0);
+  const int nci = min(256, N - ci0);
   for (int t = tg; t < taps; t += 4) {
-    float s = 0.f;
-    if (ci < nci)
-      for (int z = 0; z < splits; ++z) s += part[((int64_t)z * taps + t) * plane + (int64_t)co * N + ci0 + ci];
-    sm[ci * taps + t] = s;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (4 * c4 < nci)
+      for (int z = 0; z < splits; ++z) {
+        const float4 v = *(const float4*)(part + ((int64_t)z * taps + t) * plane + (int64_t)co * N + ci0 + 4 * c4);
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+      }
+    sm[(4 * c4 + 0) * taps + t] = s.x;
+    sm[(4 * c4 + 1) * taps + t] = s.y;
+    sm[(4 * c4 + 2) * taps + t] = s.z;
+    sm[(4 * c4 + 3) * taps + t] = s.w;
   }
   __syncthreads();
   float* o = dw + ((int64_t)co * N + ci0) * taps;
@@ -509,7 +518,7 @@ extern "C" int sad_conv_wgrad_run(const void* x, int64_t N, int32_t H, int32_t W
   SAD_REQUIRE(p.Ho > 0 && p.Wo > 0 && p.P < (1ll << 31) - 256, "wgrad: bad or too large output map");
   hipStream_t s = (hipStream_t)stream;
   SAD_REQUIRE(p.taps <= 9, "wgrad: k <= 3");
-  const dim3 rgrid((unsigned)((Cin + 63) / 64), (unsigned)Cout);
+  const dim3 rgrid((unsigned)((Cin + 255) / 256), (unsigned)Cout);
   if (p.P == 0) {  // empty batch: dW = beta*dW
     hipLaunchKernelGGL(wgrad_reduce_kernel, rgrid, dim3(256), 0, s, (const float*)nullptr, 0, p.taps, Cout, Cin, beta,
                        dw);
