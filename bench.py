@@ -48,9 +48,10 @@ BF16_PEAK_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3        # f32 MFMA = f32 vector peak (MI355X_MICROARCH.md)
 # The dominant kernel and its rocprof key in the committed PMC traffic file
 DOMINANT_VARIANT = 13
-DOMINANT_KERNEL = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1, false>|131072'
-DOMINANT_KERNEL_OLD = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1>|131072'
-TRAFFIC_JSON = os.path.join(ROOT, 'profiles', 'r01_pmc_traffic.json')
+DOMINANT_KERNEL = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1, false, false, false>|131072'
+DOMINANT_KERNEL_OLD = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1, false>|131072'
+TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r02_pmc_traffic.json', 'r01_pmc_traffic.json')
+                     if os.path.exists(os.path.join(ROOT, 'profiles', f))), '')
 FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats
 FE_BYTES = 256000 + 128512     # int16 PCM read + fp32 [128, 251] map written
 HEADS = 6
@@ -295,7 +296,7 @@ def main():
         fac = 3 if args.dtype == 'bf16x3' else 1
         alg, exe, kinfo = kernel_roofline(r, fac)
         traffic = None
-        if os.path.exists(TRAFFIC_JSON) and args.dtype == 'bf16':
+        if TRAFFIC_JSON and args.dtype == 'bf16':
             tr = json.load(open(TRAFFIC_JSON))
             rec = tr.get(DOMINANT_KERNEL) or tr.get(DOMINANT_KERNEL_OLD)
             if rec and rec.get('hbm_read_bytes') is not None:
@@ -318,7 +319,7 @@ def main():
                                    '8 launches per micro-batch of 512, about 35% of the bf16 step',
                          'achieved': round(exe, 1), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(exe / peak, 4),
                          'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, '
-                                                             'profiles/r01_pmc_traffic.json)',
+                                                             + os.path.relpath(TRAFFIC_JSON, ROOT) + ')',
                          **kinfo,
                          'backbone': {'achieved': round(bb_alg * fac, 1), 'frac': round(bb_alg * fac / peak, 4),
                                       'ms_per_step': round(r['bb_ms'], 3), 'flop_per_segment': BACKBONE_FLOP,
