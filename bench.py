@@ -79,12 +79,12 @@ def cpu_baseline(n_clips: int = 64, passes: int = 2):
     import tempfile
 
     import numpy as np
+    from oracle import audio as oaudio
     from oracle import frontend as ofe
     from oracle import resnet as ores
     from sad import weights as sw
     from sad.audio import save_pcm16
     from sad.synth import synth_segment
-    import inference_runner as ir
     sd = sw.merged_state_dict(0, 1, False, bn_stats=sw.load_bn_stats(os.path.join(ROOT, 'tests', 'golden',
                                                                                     'bn_stats_n6.npz')))
     model = ores.load_merged_state(sd)
@@ -108,10 +108,9 @@ def cpu_baseline(n_clips: int = 64, passes: int = 2):
         for i, p in enumerate(pcm):
             paths.append(os.path.join(d, f'clip{i:03d}.wav'))
             save_pcm16(paths[-1], p)
-        acfg = ir.AudioConfig()
         t0 = time.perf_counter()
         for _ in range(passes):
-            infer([ir.preprocess_waveform(p, acfg)[0] for p in paths])
+            infer([oaudio.preprocess_waveform(p)[0] for p in paths])
         t_wav = time.perf_counter() - t0
     n = n_clips * passes
     return {'value': round(n / t_mem, 2), 'unit': 'segments/s', 'cores': torch.get_num_threads(), 'kind': 'port',

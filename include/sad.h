@@ -91,6 +91,47 @@ int sad_frontend_run(const sad_frontend_plan* plan, const int16_t* pcm, int64_t 
  * mono averaging / resampling, preprocess_waveform at inference_runner.py:144-155). */
 int sad_frontend_run_f32(const sad_frontend_plan* plan, const float* wav, int64_t n_seg,
                          int64_t seg_stride, float* out_db, float* out_map, void* stream);
+/* Windows of ONE long fp32 waveform wav[wav_len], read in place: segment i
+ * starts at sample offsets[i] (DEVICE int64 array; each clamped to
+ * [0, wav_len - n_samples]).  Replaces the per-window tensors of slice_waveform
+ * (inference_runner.py:176-190) + torch.cat(specs) (:276-289): overlapping
+ * windows are never copied. */
+int sad_frontend_run_windows(const sad_frontend_plan* plan, const float* wav, int64_t wav_len,
+                             const int64_t* offsets, int64_t n_seg, float* out_db, float* out_map,
+                             void* stream);
+
+/* -------------------------------------------------------------- ingestion */
+/* preprocess_waveform (inference_runner.py:144-155) on the device: the WAV's
+ * samples go to HBM as stored (int16) or host-decoded fp32, interleaved
+ * [frames][channels]. */
+enum sad_pcm_format {
+  SAD_PCM_I16 = 0, /* int16, scaled by 1/32768 (torchaudio.load normalize=True) */
+  SAD_PCM_F32 = 1  /* fp32 (other WAV encodings, decoded on the host) */
+};
+/* out[i] = mean_c pcm[i][c] (waveform.mean(dim=0): fp32 sum x 1/C) for
+ * i < frames, 0 for frames <= i < out_len (the zero pad to one window, :151-154). */
+int sad_pcm_mono_run(const void* pcm, int32_t format, int64_t frames, int32_t channels, float* out,
+                     int64_t out_len, void* stream);
+
+/* Replaces torchaudio.transforms.Resample(orig_freq, new_freq) with its
+ * defaults (sinc_interp_hann, lowpass_filter_width 6, rolloff 0.99), as built
+ * at inference_runner.py:148 (and submodel_trainer.py:150-153): the plan holds
+ * the polyphase kernel table (float64 on the host, rounded once to fp32). */
+typedef struct sad_resample_plan sad_resample_plan;
+int sad_resample_plan_create(int32_t orig_freq, int32_t new_freq, sad_resample_plan** out);
+int sad_resample_plan_destroy(sad_resample_plan* plan);
+/* ceil(new * n_in / orig) with the rates reduced by their gcd (torchaudio's target_length) */
+int sad_resample_out_len(const sad_resample_plan* plan, int64_t n_in, int64_t* n_out);
+/* x [n_in] fp32 -> y [y_len] fp32: the resampled signal, then zeros up to
+ * y_len (>= sad_resample_out_len) */
+int sad_resample_run(const sad_resample_plan* plan, const float* x, int64_t n_in, float* y, int64_t y_len,
+                     void* stream);
+
+/* out[w] = max |wav[w*hop, w*hop + window)| (window clipped at n; NaN
+ * propagates as in torch.max), w < n_windows: the silence test of
+ * slice_waveform (inference_runner.py:182-184) without moving windows to the host. */
+int sad_window_absmax_run(const float* wav, int64_t n, int64_t window, int64_t hop, int64_t n_windows,
+                          float* out, void* stream);
 
 /* Replaces torchvision.transforms.Resize((512,512)) + repeat(3,1,1)
  * (inference_runner.py:172-174) for callers that want the image itself:

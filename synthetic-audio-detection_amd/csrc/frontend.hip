@@ -102,7 +102,9 @@ constexpr int FE_MAX_NNZ = 1600;    // mel weights in LDS (1515 for the referenc
 
 template <typename IT>  // int16_t PCM (scaled by 1/32768, torchaudio.load normalize) or float
 __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
-    const IT* __restrict__ pcm, int64_t seg_stride, int n_samples, int n_frames, int hop,
+    const IT* __restrict__ pcm, int64_t seg_stride, const int64_t* __restrict__ seg_offs, int64_t max_off,
+    int n_samples,
+    int n_frames, int hop,
     const float2* __restrict__ tw1024, const float* __restrict__ window, const int* __restrict__ mel_start,
     const int* __restrict__ mel_len, const int* __restrict__ mel_off, const float* __restrict__ mel_w, int nnz,
     int n_mels, int bin_lo, int bin_hi, float* __restrict__ out) {
@@ -115,7 +117,15 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t seg = blockIdx.y;
-  const IT* x = pcm + seg * seg_stride;
+  // segment `seg` starts at sample seg_offs[seg] (windows of a long waveform,
+  // sad_frontend_run_windows) or at seg * seg_stride
+  // (offsets are clamped to [0, max_off]: a bad table cannot read out of bounds)
+  int64_t x0 = seg * seg_stride;
+  if (seg_offs) {
+    const int64_t o = seg_offs[seg];
+    x0 = o < 0 ? 0 : (o > max_off ? max_off : o);
+  }
+  const IT* x = pcm + x0;
   const float in_scale = sizeof(IT) == 2 ? (1.0f / 32768.0f) : 1.0f;
   const bool staged = n_mels <= FE_STAGE_MELS && bin_hi - bin_lo < FE_POW && nnz <= FE_MAX_NNZ;
   for (int i = tid; i < FE_NC; i += 256) s_tw[i] = tw1024[i];
@@ -501,11 +511,12 @@ extern "C" int sad_frontend_frames(const sad_frontend_plan* p, int32_t* n) {
 
 template <typename IT>
 static int frontend_run(const sad_frontend_plan* p, const IT* pcm, int64_t n_seg, int64_t seg_stride,
-                        float* out_db, float* out_map, void* stream) {
+                        const int64_t* seg_offs, int64_t max_off, float* out_db, float* out_map,
+                        void* stream) {
   SAD_REQUIRE(p, "null plan");
   SAD_REQUIRE(n_seg >= 0, "n_seg < 0");
   SAD_REQUIRE(out_map, "out_map is required");
-  SAD_REQUIRE(seg_stride >= p->cfg.n_samples, "seg_stride < n_samples");
+  SAD_REQUIRE(seg_offs || seg_stride >= p->cfg.n_samples, "seg_stride < n_samples");
   if (n_seg == 0) return SAD_OK;
   SAD_REQUIRE(pcm, "null pcm");
   hipStream_t s = (hipStream_t)stream;
@@ -516,9 +527,10 @@ static int frontend_run(const sad_frontend_plan* p, const IT* pcm, int64_t n_seg
     const int64_t chunk = std::min<int64_t>(65535, n_seg - done);
     const size_t off = (size_t)done * p->cfg.n_mels * p->n_frames;
     hipLaunchKernelGGL(fe_mel_db_kernel<IT>, dim3(n_fb, (unsigned)chunk), dim3(256), 0, s,
-                       pcm + done * seg_stride, seg_stride, p->cfg.n_samples, p->n_frames,
-                       p->cfg.hop_length, p->d_tw1024, p->d_window, p->d_mel_start, p->d_mel_len,
-                       p->d_mel_off, p->d_mel_w, p->nnz, p->cfg.n_mels, p->bin_lo, p->bin_hi, dbbuf + off);
+                       seg_offs ? pcm : pcm + done * seg_stride, seg_stride, seg_offs ? seg_offs + done : nullptr,
+                       max_off, p->cfg.n_samples, p->n_frames, p->cfg.hop_length, p->d_tw1024, p->d_window,
+                       p->d_mel_start, p->d_mel_len, p->d_mel_off, p->d_mel_w, p->nnz, p->cfg.n_mels, p->bin_lo,
+                       p->bin_hi, dbbuf + off);
     SAD_CHECK_HIP(hipGetLastError());
     hipLaunchKernelGGL(fe_normalize_kernel, dim3((unsigned)chunk), dim3(1024), 0, s, dbbuf + off,
                        p->cfg.n_mels * p->n_frames, p->cfg.top_db, out_map + off);
@@ -530,12 +542,23 @@ static int frontend_run(const sad_frontend_plan* p, const IT* pcm, int64_t n_seg
 
 extern "C" int sad_frontend_run(const sad_frontend_plan* p, const int16_t* pcm, int64_t n_seg,
                                 int64_t seg_stride, float* out_db, float* out_map, void* stream) {
-  return frontend_run(p, pcm, n_seg, seg_stride, out_db, out_map, stream);
+  return frontend_run(p, pcm, n_seg, seg_stride, nullptr, 0, out_db, out_map, stream);
 }
 
 extern "C" int sad_frontend_run_f32(const sad_frontend_plan* p, const float* wav, int64_t n_seg,
                                     int64_t seg_stride, float* out_db, float* out_map, void* stream) {
-  return frontend_run(p, wav, n_seg, seg_stride, out_db, out_map, stream);
+  return frontend_run(p, wav, n_seg, seg_stride, nullptr, 0, out_db, out_map, stream);
+}
+
+extern "C" int sad_frontend_run_windows(const sad_frontend_plan* p, const float* wav, int64_t wav_len,
+                                        const int64_t* offsets, int64_t n_seg, float* out_db, float* out_map,
+                                        void* stream) {
+  SAD_REQUIRE(p, "null plan");
+  SAD_REQUIRE(wav_len >= p->cfg.n_samples, "waveform shorter than one segment");
+  SAD_REQUIRE(n_seg == 0 || offsets, "null offsets");
+  // the offsets live on the device (not checked here); the kernel clamps each
+  // to [0, wav_len - n_samples]
+  return frontend_run(p, wav, n_seg, 0, offsets, wav_len - p->cfg.n_samples, out_db, out_map, stream);
 }
 
 extern "C" int sad_resize_run(const float* map, int64_t n, int32_t h, int32_t w, int32_t oh,

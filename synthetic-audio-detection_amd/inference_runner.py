@@ -8,12 +8,15 @@ Reference map (file:line in modular/source/inference_runner.py):
   ModularMultiHeadClassifier  :53-73   -> device engine; forward returns [B, N+1]
   load_merged_model           :77-123  -> same key mapping / ValueError / sorted indices
   AudioConfig, SpectrogramConfig :127-142
-  preprocess_waveform         :144-155 -> sad.audio.load (+ resample), mono, zero-pad
+  preprocess_waveform         :144-155 -> on the device (sad.ingest): WAV samples
+                                           uploaded as stored, mono, resample, zero-pad
   waveform_to_spectrogram     :157-174 -> fused HIP front end + resize, [1,3,512,512]
   slice_waveform              :176-190 -> identical host logic
   interpret_multihead_logits  :194-214 -> identical host logic (torch CPU fp32)
-  main                        :218-353 -> same flow; windows are batched through the
-                                           device front end and the ensemble
+  main                        :218-353 -> same flow; the file is decoded, resampled and
+                                           windowed on the device (windows read in
+                                           place by the front end), batched through
+                                           the ensemble
 
 Differences (documented in DESIGN.md):
   * no CPU fallback: ``--device`` must name an MI355X (the reference silently
@@ -47,6 +50,7 @@ if _HERE not in sys.path:
 
 from sad import audio as _audio  # noqa: E402
 from sad import engine as _engine  # noqa: E402
+from sad import ingest as _ingest  # noqa: E402
 from sad import weights as _weights  # noqa: E402
 
 
@@ -223,19 +227,14 @@ class SpectrogramConfig:
     norm: str = 'slaney'
 
 
-def preprocess_waveform(path: str, cfg: AudioConfig):
-    """inference_runner.py:144-155 -> (mono fp32 [T], sr)."""
-    wf, sr = _audio.load(path)
-    wf = wf.mean(dim=0)
-    if sr != cfg.sample_rate:
-        wf = _audio.resample(wf, sr, cfg.sample_rate)
-        sr = cfg.sample_rate
-    needed = int(cfg.window_size * sr)
-    if wf.shape[0] < needed:
-        temp = torch.zeros(needed)
-        temp[:wf.shape[0]] = wf
-        wf = temp
-    return wf, sr
+def preprocess_waveform(path: str, cfg: AudioConfig, device='cuda'):
+    """inference_runner.py:144-155 -> (mono fp32 [T], sr), computed on the
+    device (csrc/ingest.hip): the WAV's samples are uploaded as stored (int16),
+    averaged to mono, resampled to cfg.sample_rate when the file differs
+    (torchaudio Resample semantics) and zero-padded to one window.  The
+    waveform stays on the device."""
+    needed = int(cfg.window_size * cfg.sample_rate)
+    return _ingest.load_waveform(path, cfg.sample_rate, needed, _engine._dev(device))
 
 
 _FE_CACHE = {}
@@ -339,8 +338,19 @@ def summarize(filename, outputs, timestamps, threshold, synthetic_names, real_na
 def run_windows(model: ModularMultiHeadClassifier, chunks, sr: int, spec_cfg: SpectrogramConfig,
                 batch_size: int = 128) -> torch.Tensor:
     """All windows -> [n, N+1] merged logits (fp32, host): device front end +
-    ensemble, `batch_size` windows per launch (the reference's mini-batch, :284)."""
+    ensemble, `batch_size` windows per launch (the reference's mini-batch, :284).
+    `chunks` is a list of window tensors (slice_waveform's) or a
+    sad.ingest.Windows, whose windows the front end reads in place from the
+    device waveform."""
     dev = model.device
+    if isinstance(chunks, _ingest.Windows):
+        fe = _frontend(dev, spec_cfg, chunks.window, sr)
+        wf = chunks.wf.to(dev)
+        offs = chunks.offsets.to(dev)
+        outs = []
+        for start in range(0, len(chunks), batch_size):
+            outs.append(model.forward_maps(fe.windows(wf, offs[start:start + batch_size])).cpu())
+        return torch.cat(outs)
     fe = _frontend(dev, spec_cfg, chunks[0].shape[0], sr)
     outs = []
     for start in range(0, len(chunks), batch_size):
@@ -386,14 +396,18 @@ def main(argv=None):
     audio_cfg = AudioConfig(sample_rate=32000, window_size=4.0, overlap=0.0, silence_threshold=1e-3)
     spec_cfg = SpectrogramConfig(n_fft=2048, hop_length=512, n_mels=128, f_min=20, f_max=12000, top_db=80,
                                  norm='slaney')
-    wf, sr = preprocess_waveform(args.audio, audio_cfg)
-    chunks, timestamps = slice_waveform(wf, sr, audio_cfg)
-    if not chunks:
+    wf, sr = preprocess_waveform(args.audio, audio_cfg, device)
+    # slice_waveform (:176-190) on the device: the silence test per window runs
+    # there, the kept windows are read in place by the front end
+    starts, timestamps = _ingest.select_windows(wf, sr, audio_cfg.window_size, audio_cfg.overlap,
+                                                audio_cfg.silence_threshold)
+    if not starts:
         print('No valid audio chunks found (all below silence threshold). Exiting.')
         out = {'filename': args.audio, 'segments': [], 'percentages': {}}
         with open(args.output_json, 'w', encoding='utf-8') as f:
             json.dump(out, f, indent=4)
         return out
+    chunks = _ingest.Windows(wf, starts, int(audio_cfg.window_size * sr))
     outputs = run_windows(model, chunks, sr, spec_cfg, args.batch_size)
     out_json = summarize(args.audio, outputs, timestamps, args.threshold, synthetic_names, real_name,
                          args.smooth, audio_cfg.window_size)

@@ -22,6 +22,8 @@ SAD_F32 = 0
 SAD_BF16 = 1
 SAD_BF16X3 = 2  # split-bf16 parity mode (include/sad.h)
 DTYPES = {'fp32': SAD_F32, 'bf16': SAD_BF16, 'bf16x3': SAD_BF16X3}
+SAD_PCM_I16 = 0  # sad_pcm_format
+SAD_PCM_F32 = 1
 
 # name -> (restype, argtypes); exactly the symbols include/sad.h declares.
 P = ctypes.c_void_p
@@ -52,7 +54,15 @@ SIGNATURES = {
     'sad_frontend_frames': (ctypes.c_int, [P, ctypes.POINTER(I32)]),
     'sad_frontend_run': (ctypes.c_int, [P, P, I64, I64, P, P, P]),
     'sad_frontend_run_f32': (ctypes.c_int, [P, P, I64, I64, P, P, P]),
+    'sad_frontend_run_windows': (ctypes.c_int, [P, P, I64, P, I64, P, P, P]),
     'sad_resize_run': (ctypes.c_int, [P, I64, I32, I32, I32, I32, I32, P, P]),
+    # ingestion (include/sad.h "ingestion")
+    'sad_pcm_mono_run': (ctypes.c_int, [P, I32, I64, I32, P, I64, P]),
+    'sad_resample_plan_create': (ctypes.c_int, [I32, I32, ctypes.POINTER(P)]),
+    'sad_resample_plan_destroy': (ctypes.c_int, [P]),
+    'sad_resample_out_len': (ctypes.c_int, [P, I64, ctypes.POINTER(I64)]),
+    'sad_resample_run': (ctypes.c_int, [P, P, I64, P, I64, P]),
+    'sad_window_absmax_run': (ctypes.c_int, [P, I64, I64, I64, I64, P, P]),
     'sad_backbone_plan_create': (ctypes.c_int, [FPP, I32, I32, I32, I32, ctypes.POINTER(P)]),
     'sad_backbone_plan_destroy': (ctypes.c_int, [P]),
     'sad_backbone_workspace_size': (ctypes.c_int, [P, I64, ctypes.POINTER(SZ)]),

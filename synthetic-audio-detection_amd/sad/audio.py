@@ -12,9 +12,9 @@ these are restatements of its documented behaviour:
 * ``resample(wf, orig, new)`` -> torchaudio.functional.resample with its
   defaults (sinc_interp_hann, lowpass_filter_width=6, rolloff=0.99): windowed
   sinc kernel built in float64, cast to float32, applied as a strided conv1d.
-
-Host (CPU) work in the reference too: it happens once per file, before the
-device hot path.
+  Used only by the trainer's Dataset, which runs in DataLoader worker
+  processes on the host, as the reference's does (submodel_trainer.py:143-153).
+  The inference path resamples on the device (sad.ingest, csrc/ingest.hip).
 """
 from __future__ import annotations
 
@@ -43,8 +43,11 @@ def _read_chunks(data: bytes):
     return fmt, payload
 
 
-def load(path: str):
-    """torchaudio.load(path) for WAV files -> (Tensor[C, T] float32, sample_rate)."""
+def read_wav(path: str):
+    """WAV -> (interleaved samples [frames * channels], channels, sample_rate).
+    16-bit PCM stays int16 as stored (the device scales it, sad_pcm_mono_run);
+    every other encoding is decoded to float32 with torchaudio.load's
+    normalize=True scaling."""
     with open(path, 'rb') as f:
         data = f.read()
     fmt, payload = _read_chunks(data)
@@ -58,7 +61,7 @@ def load(path: str):
         if bits == 8:
             x = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128.0) / 128.0
         elif bits == 16:
-            x = np.frombuffer(raw, '<i2').astype(np.float32) / 32768.0
+            x = np.frombuffer(raw, '<i2').copy()
         elif bits == 24:
             b = np.frombuffer(raw, np.uint8).reshape(-1, 3).astype(np.int32)
             v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
@@ -72,7 +75,15 @@ def load(path: str):
         x = np.frombuffer(raw, '<f4' if bits == 32 else '<f8').astype(np.float32)
     else:
         raise ValueError(f'unsupported WAV format tag {tag:#x}')
-    return torch.from_numpy(x.reshape(n, ch).T.copy()), sr
+    return x, ch, sr
+
+
+def load(path: str):
+    """torchaudio.load(path) for WAV files -> (Tensor[C, T] float32, sample_rate)."""
+    x, ch, sr = read_wav(path)
+    if x.dtype == np.int16:
+        x = x.astype(np.float32) / 32768.0
+    return torch.from_numpy(x.reshape(-1, ch).T.copy()), sr
 
 
 def load_pcm16_mono(path: str):
@@ -110,7 +121,7 @@ def _sinc_resample_kernel(orig: int, new: int, gcd: int, lowpass_filter_width: i
     t = t * math.pi
     scale = base / orig
     kernels = torch.where(t == 0, torch.tensor(1.0).to(t), t.sin() / t)
-    kernels = kernels * window * scale
+    kernels = kernels * (window * scale)  # torchaudio: kernels *= window * scale
     return kernels.to(torch.float32), width
 
 

@@ -110,6 +110,23 @@ class FrontEnd:
                       _lib.stream_handle(self.device))
         return (out, db) if want_db else out
 
+    def windows(self, wf: torch.Tensor, offsets: torch.Tensor, want_db: bool = False,
+                out: torch.Tensor | None = None):
+        """Windows of one long fp32 waveform wf [T] on the device, segment i at
+        sample offsets[i] (int64 device tensor), read in place
+        (sad_frontend_run_windows) -> map [n, n_mels, frames]."""
+        assert wf.dtype == torch.float32 and wf.dim() == 1 and wf.is_contiguous() and wf.device == self.device
+        assert offsets.dtype == torch.int64 and offsets.dim() == 1 and offsets.is_contiguous()
+        assert offsets.device == self.device and wf.shape[0] >= self.n_samples
+        n = offsets.shape[0]
+        if out is None:
+            out = torch.empty(n, self.n_mels, self.n_frames, device=self.device, dtype=torch.float32)
+        db = torch.empty_like(out) if want_db else None
+        with torch.cuda.device(self.device):
+            _lib.call('sad_frontend_run_windows', self._plan, _lib.ptr(wf), wf.shape[0], _lib.ptr(offsets), n,
+                      _lib.ptr(db), _lib.ptr(out), _lib.stream_handle(self.device))
+        return (out, db) if want_db else out
+
     def __del__(self):
         try:
             if getattr(self, '_plan', None):

@@ -71,12 +71,72 @@ def test_resample_kernel_matches_torchaudio_formula():
     assert torch.allclose(k[width - 3], k[width + 3], atol=1e-7)
 
 
-def test_preprocess_waveform_mono_pad(tmp_path):
-    import inference_runner as ir
+def test_oracle_preprocess_waveform_mono_pad(tmp_path):
+    """oracle preprocess_waveform (scipy WAV decode, torch mean, pad) on a stereo int16 file."""
+    from oracle import audio as oaudio
     x = (np.random.RandomState(1).randn(2, 5000) * 1000).astype(np.int16)
     p = tmp_path / 's.wav'
     _write(p, x, 32000, 2)
-    wf, sr = ir.preprocess_waveform(str(p), ir.AudioConfig())
+    wf, sr = oaudio.preprocess_waveform(str(p))
     assert sr == 32000 and wf.shape == (128000,)
     assert torch.equal(wf[:5000], torch.from_numpy(x.astype(np.float32) / 32768.0).mean(0))
     assert torch.count_nonzero(wf[5000:]) == 0
+
+
+def test_oracle_wav_decoders_agree(tmp_path):
+    """scipy's WAV reader (oracle) and sad.audio.read_wav / load decode 8/16/24/32-bit alike."""
+    from oracle import audio as oaudio
+    rs = np.random.RandomState(5)
+    cases = [(1, rs.randint(0, 256, (2, 300))), (2, rs.randint(-32768, 32768, (1, 300))),
+             (3, rs.randint(-(1 << 23), 1 << 23, (2, 300))), (4, rs.randint(-(1 << 31), (1 << 31) - 1, (1, 300)))]
+    for width, x in cases:
+        p = tmp_path / f'w{width}.wav'
+        _write(p, x, 22050, width)
+        a, sra = audio.load(str(p))
+        b, srb = oaudio.load(str(p))
+        assert sra == srb == 22050 and a.shape == b.shape
+        assert torch.equal(a, b), width
+        raw, ch, sr = audio.read_wav(str(p))
+        assert ch == x.shape[0] and sr == 22050 and raw.dtype == (np.int16 if width == 2 else np.float32)
+
+
+RATES = [(44100, 32000), (48000, 32000), (16000, 32000), (22050, 32000), (8000, 32000), (96000, 32000)]
+
+
+def test_oracle_resample_polyphase_vs_direct():
+    """torchaudio's polyphase form (oracle.resample, fp32 conv1d) against the
+    defining float64 sum (oracle.resample_direct): pins the polyphase index
+    arithmetic that the HIP kernel shares; also the trainer's host resample."""
+    from oracle import audio as oaudio
+    rs = np.random.RandomState(2)
+    for orig, new in RATES:
+        x = (rs.randn(3001) * 0.3).astype(np.float32)
+        ref = oaudio.resample_direct(x, orig, new)
+        y = oaudio.resample(torch.from_numpy(x), orig, new).double().numpy()
+        assert y.shape == ref.shape == (math.ceil(new * 3001 / orig),)
+        # torchaudio forms the phase -p/new in fp32 (its arange / new), which moves
+        # the taps by ~1e-5 against the exact float64 sum; an indexing error would be O(0.1)
+        assert np.abs(y - ref).max() < 5e-5, (orig, new, np.abs(y - ref).max())
+        h = audio.resample(torch.from_numpy(x), orig, new).double().numpy()
+        assert np.array_equal(h, y), (orig, new)
+
+
+def test_oracle_kernel_table_equals_host():
+    from oracle import audio as oaudio
+    for orig, new in RATES:
+        g = math.gcd(orig, new)
+        k1, w1 = oaudio._kernel(orig // g, new // g)
+        k2, w2 = audio._sinc_resample_kernel(orig, new, g)
+        assert w1 == w2 and torch.equal(k1, k2)
+
+
+def test_window_starts_match_slice_waveform():
+    import inference_runner as ir
+    from sad import ingest
+    cfg = ir.AudioConfig(overlap=0.85)
+    for n in (128000, 128001, 140000, 500000, 127999):
+        wf = torch.ones(n)
+        chunks, ts = ir.slice_waveform(wf, 32000, cfg)
+        window = int(cfg.window_size * 32000)
+        starts = list(ingest.window_starts(n, window, int((1 - cfg.overlap) * window)))
+        assert [s / 32000 for s in starts] == ts
