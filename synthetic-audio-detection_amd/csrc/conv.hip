@@ -457,6 +457,8 @@ constexpr int STEM_P = 8;
 constexpr int STEM_BAND_ROWS = 4 * STEM_P + 8;  // 4P+7 with non-zero weights
 constexpr int STEM_BPITCH = 544;                 // bf16 elements per band row (>= 518)
 constexpr int STEM_HROWS = 12;                   // x-interpolated map rows kept in LDS (>= 4P+8 image rows at 128/512)
+constexpr int STEM_UPITCH = 520;                 // floats per x-interpolated row, indexed by band column
+                                                 // (>= 518 read; zero outside the image)
 constexpr int STEM_OPITCH = 160;                 // staging bytes per pooled pixel (64 ch bf16 + pad):
                                                  // 40 dwords -> the 4 rows a 32-lane group writes
                                                  // land on disjoint 8-bank sets
@@ -471,11 +473,14 @@ __device__ __forceinline__ float dppf(float v) {
 // W_hi.X_lo, and the pooled output is stored split ([hi 32 | lo 32] per 32
 // channels; one workgroup per CU for the larger LDS footprint).
 constexpr int STEM_OPITCH_X3 = 288;  // 128 bf16 (64 ch hi + lo) + pad: 72 dwords -> 4 rows on disjoint bank sets
+// s_u holds, while the band is built, the x-interpolated rows + a zero row +
+// the [NBR] row table; afterwards the pooled-row staging + the wave-edge exchange
+constexpr int stem_u_build_floats() { return (STEM_HROWS + 1) * STEM_UPITCH + 4 * STEM_BAND_ROWS; }
 template <bool X3>
 constexpr int stem_u_floats() {
-  return X3 ? (128 * STEM_OPITCH_X3 / 4 + 256 > STEM_HROWS * 512 + 256 ? 128 * STEM_OPITCH_X3 / 4 + 256
-                                                                         : STEM_HROWS * 512 + 256)
-            : STEM_HROWS * 512 + 256;
+  return (X3 ? 128 * STEM_OPITCH_X3 / 4 : 128 * STEM_OPITCH / 4) + 256 > stem_u_build_floats()
+             ? (X3 ? 128 * STEM_OPITCH_X3 / 4 : 128 * STEM_OPITCH / 4) + 256
+             : stem_u_build_floats();
 }
 
 // TRAIN (the trainer's bf16 stem, submodel_trainer.py:250-255 in model.train()):
@@ -557,9 +562,17 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
     src_row(iy_hi, t1, yhi, tl);
     const int nh = yhi - ylo + 1;
     if (nh <= STEM_HROWS) {
-      // x-lerp of map rows ylo..yhi for every image column: a thread owns
-      // columns tid and tid + 256 and issues all its rows' gathers before the
-      // first use (one memory latency per workgroup instead of one per row)
+      // separable resize in two vector passes.  (1) x-lerp of map rows
+      // ylo..yhi into s_u, indexed by BAND column tc = ix + 3 (zero outside
+      // the image): a thread owns image columns tid and tid + 256 and issues
+      // all its rows' gathers before the first use (one memory latency per
+      // workgroup).  (2) y-lerp of 4 band columns per item from a per-row table
+      // (source-row offsets and weights; rows outside the image point at a zero
+      // row), so the band costs 2 ds_read_b128 + 8 VALU + one 8-B store per 4
+      // pixels instead of the per-pixel index arithmetic
+      constexpr int UP = STEM_UPITCH;
+      float* s_zero = s_u + STEM_HROWS * UP;
+      int4* s_rt = (int4*)(s_u + (STEM_HROWS + 1) * UP);
       int x0[2], x1[2];
       float lx[2];
 #pragma unroll
@@ -585,21 +598,49 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
       for (int r = 0; r < STEM_HROWS; ++r)
         if (r < nh) {
 #pragma unroll
-          for (int c = 0; c < 2; ++c) s_u[r * 512 + tid + 256 * c] = (1.f - lx[c]) * g0[r][c] + lx[c] * g1[r][c];
+          for (int c = 0; c < 2; ++c) s_u[r * UP + 3 + tid + 256 * c] = (1.f - lx[c]) * g0[r][c] + lx[c] * g1[r][c];
         }
-      __syncthreads();
-#pragma unroll 4
-      for (int i = tid; i < NBR * STEM_BPITCH; i += 256) {
-        const int tr = i / STEM_BPITCH, tc = i - tr * STEM_BPITCH;
-        const int iy = 4 * py0 - 5 + tr, ix = tc - 3;
-        float v = 0.f;
-        if ((unsigned)iy < 512u && (unsigned)ix < 512u) {
+      // band columns outside the image (tc 0..2 and 515..519) of every row, the zero row
+      if (tid < STEM_HROWS * 8) {
+        const int r = tid >> 3, k = tid & 7;
+        s_u[r * UP + (k < 3 ? k : 512 + k)] = 0.f;
+      }
+      for (int i = tid; i < UP; i += 256) s_zero[i] = 0.f;
+      if (tid < NBR) {
+        const int iy = 4 * py0 - 5 + tid;
+        int4 rt = make_int4(STEM_HROWS * UP, STEM_HROWS * UP, __float_as_int(1.f), __float_as_int(0.f));
+        if ((unsigned)iy < 512u) {
           int y0, y1;
           float ly;
           src_row(iy, y0, y1, ly);
-          v = (1.f - ly) * s_u[(y0 - ylo) * 512 + ix] + ly * s_u[(y1 - ylo) * 512 + ix];
+          rt = make_int4((y0 - ylo) * UP, (y1 - ylo) * UP, __float_as_int(1.f - ly), __float_as_int(ly));
         }
-        put(i, v);
+        s_rt[tid] = rt;
+      }
+      __syncthreads();
+      constexpr int QPR = (2 * 255 + 8 + 3) / 4;  // 4-column quads per band row that fragments read (tc < 518)
+      static_assert(4 * QPR <= UP && 4 * QPR <= STEM_BPITCH, "band quads");
+#pragma unroll 2
+      for (int it = tid; it < NBR * QPR; it += 256) {
+        const int tr = it / QPR, q = it - tr * QPR;
+        const int4 rt = s_rt[tr];
+        const float w0 = __int_as_float(rt.z), w1 = __int_as_float(rt.w);
+        const float4 u0 = *(const float4*)(s_u + rt.x + 4 * q);
+        const float4 u1 = *(const float4*)(s_u + rt.y + 4 * q);
+        const float v[4] = {w0 * u0.x + w1 * u1.x, w0 * u0.y + w1 * u1.y, w0 * u0.z + w1 * u1.z,
+                            w0 * u0.w + w1 * u1.w};
+        u16 h[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = f2bf(v[e]);
+        const int o = tr * STEM_BPITCH + 4 * q;
+        *(uint2*)(s_img + o) = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+        if constexpr (X3) {
+          u16 l[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) l[e] = f2bf(v[e] - bf2f(h[e]));
+          *(uint2*)(s_imgl + o) =
+              make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
+        }
       }
     } else {  // very tall maps: direct bilinear per pixel
       for (int i = tid; i < NBR * STEM_BPITCH; i += 256) {
