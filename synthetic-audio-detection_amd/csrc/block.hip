@@ -157,13 +157,18 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   }
 
   // ---- issue-side state: pixel-row metadata of the tile being DMA'd
-  int poff0[QP], poff1[QP], piy[QP], pix[QP];
+  // LEAN (8 pixel pieces per wave: variants 16, 19): per piece one row offset
+  // and a tap-validity mask (bit ky*KW + kx) instead of the source row/column
+  // and the shortcut offset (recomputed on its few K-steps), 16 VGPRs fewer
+  constexpr bool LEAN = QP > 4;
+  int poff0[QP], poff1[LEAN ? 1 : QP], piy[LEAN ? 1 : QP], pix[LEAN ? 1 : QP];
+  unsigned pmask[LEAN ? QP : 1];
   int itile = tp_begin;
   // K cursor of the next DMA, kept incrementally (no scalar divisions per step):
   // step iks = (ky * KW + kx) * kpt + ci of the conv taps, then the shortcut.
   // (Channel-chunk-outer order -- consecutive steps re-reading one 64-channel
   // slice shifted by a tap -- measured 2-4 % slower on layer3/4.)
-  int iks = 0, ici = 0, ikx = 0, iky = 0, itoff = 0;
+  int iks = 0, ici = 0, ikx = 0, iky = 0, itoff = 0, itap = 0;
   const int kpt = a.Cin * ES / 128;  // K-steps per tap
   auto set_tile = [&](int tp) __attribute__((always_inline)) {
 #pragma unroll
@@ -175,17 +180,42 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
         const int b = (int)((unsigned)m / (unsigned)HoWo);
         const int rem = m - b * HoWo;
         const int oy = (int)((unsigned)rem / (unsigned)a.Wo), ox = rem - oy * a.Wo;
-        piy[i] = oy * a.stride - a.pad;
-        pix[i] = ox * a.stride - a.pad;
-        poff0[i] = ((b * a.H + piy[i]) * a.W + pix[i]) * ps0 + c * 16;
-        poff1[i] = ((b * a.H1 + oy * a.ss1) * a.W1 + ox * a.ss1) * ps1 + c * 16;
+        const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
+        poff0[i] = ((b * a.H + iy0) * a.W + ix0) * ps0 + c * 16;
+        if constexpr (LEAN) {
+          unsigned mk = 0;
+          for (int ky = 0; ky < a.KH; ++ky)
+            for (int kx = 0; kx < a.KW; ++kx)
+              if ((unsigned)(iy0 + ky) < (unsigned)a.H && (unsigned)(ix0 + kx) < (unsigned)a.W)
+                mk |= 1u << (ky * a.KW + kx);
+          pmask[i] = mk;
+        } else {
+          piy[i] = iy0;
+          pix[i] = ix0;
+          poff1[i] = ((b * a.H1 + oy * a.ss1) * a.W1 + ox * a.ss1) * ps1 + c * 16;
+        }
       } else {
-        piy[i] = -0x4000;
-        pix[i] = -0x4000;
         poff0[i] = 0;
-        poff1[i] = 0x7FFF0000;  // + K offset (< 64 KB) stays past num_records
+        if constexpr (LEAN) {
+          pmask[i] = 0;
+        } else {
+          piy[i] = -0x4000;
+          pix[i] = -0x4000;
+          poff1[i] = 0x7FFF0000;  // + K offset (< 64 KB) stays past num_records
+        }
       }
     }
+  };
+  // LEAN: the shortcut source offset of piece k of tile tp
+  auto shortcut_off = [&](int tp, int k) __attribute__((always_inline)) {
+    const int r = 8 * (wave + NW * k) + lrow;
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int m = tp * BP + r;
+    if (m >= M) return 0x7FFF0000;
+    const int b = (int)((unsigned)m / (unsigned)HoWo);
+    const int rem = m - b * HoWo;
+    const int oy = (int)((unsigned)rem / (unsigned)a.Wo), ox = rem - oy * a.Wo;
+    return ((b * a.H1 + oy * a.ss1) * a.W1 + ox * a.ss1) * ps1 + c * 16;
   };
   set_tile(itile);
   // the tile's bias, behind the ring stages (published by the first barrier);
@@ -201,11 +231,17 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
     const unsigned sb = lds0 + st * STAGE;
     if (k < QP) {
       if (iks < nk0) {
-        const int iy = piy[k] + iky, ix = pix[k] + ikx;
-        const bool ok = ((unsigned)iy < (unsigned)a.H) && ((unsigned)ix < (unsigned)a.W);
+        bool ok;
+        if constexpr (LEAN) {
+          ok = (pmask[k] >> itap) & 1u;
+        } else {
+          const int iy = piy[k] + iky, ix = pix[k] + ikx;
+          ok = ((unsigned)iy < (unsigned)a.H) && ((unsigned)ix < (unsigned)a.W);
+        }
         dma16_m0(r0, ok ? poff0[k] + itoff : 0x7FFFFFF0, sb + (wave + NW * k) * 1024);
       } else {
-        dma16_m0(r1, poff1[k] + (iks - nk0) * 128, sb + (wave + NW * k) * 1024);
+        const int o1 = LEAN ? shortcut_off(itile, k) : poff1[LEAN ? 0 : k];
+        dma16_m0(r1, o1 + (iks - nk0) * 128, sb + (wave + NW * k) * 1024);
       }
     } else {
       dma16_m0(rw, woff[k - QP] + iks * 128, sb + BP * 128 + (wave + NW * (k - QP)) * 1024);
@@ -217,6 +253,7 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
       itoff += 128;
       if (++ici == kpt) {
         ici = 0;
+        ++itap;
         itoff += ps0 - kpt * 128;
         if (++ikx == a.KW) {
           ikx = 0;
@@ -226,7 +263,7 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
       }
     }
     if (++iks == nk) {
-      iks = ici = ikx = iky = itoff = 0;
+      iks = ici = ikx = iky = itoff = itap = 0;
       if (++itile < tp_end) set_tile(itile);
     }
   };
@@ -572,6 +609,7 @@ static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
   static_assert(!ST_OK || block_smem_bytes_st<WC, WP, TC, TP, S, OCC>() * OCC <= 160 * 1024, "LDS budget (ST)");
   const int smem = a.st_part ? block_smem_bytes_st<WC, WP, TC, TP, S, OCC>() : smem0;
   SAD_REQUIRE(RES_OK || !a.res, "this block-conv variant has no epilogue residual (variants 13, 20, 21, 25 do)");
+  SAD_REQUIRE(16 * TP * WP / 8 / (WC * WP) <= 4 || a.KH * a.KW <= 32, "variants 16 / 19: at most 32 filter taps");
   const void* kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3>;
   if constexpr (RES_OK) {
     if (a.res) kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true, X3>;
@@ -631,6 +669,8 @@ static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
 // 13: 256x256 8w 128x64 S2 128 KB 1     14: 128x256 8w 64x64  S2  96 KB 1
 // 15: 128x256 8w 64x64  S3 144 KB 1     16: 64x512  8w 64x64  S2 144 KB 1
 // 17: 256x128 4w 128x64 S2  96 KB 1     18: 128x256 4w 64x128 S2  96 KB 1
+// 19: 128x512 8w 128x64 S2 160 KB 1 (Cout 128: the 256x256 kernel's wave tile and
+//     LDS fill per FLOP within 20 %; the bias is read from global, no LDS left)
 template <typename T, bool X3 = false>
 static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
   switch (v) {
@@ -644,6 +684,7 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
     case 16: return launch_block_t<T, 1, 8, 4, 4, 2, 1, false, X3>(a, s);
     case 17: return launch_block_t<T, 2, 2, 8, 4, 2, 1, false, X3>(a, s);
     case 18: return launch_block_t<T, 2, 2, 4, 8, 2, 1, false, X3>(a, s);
+    case 19: return launch_block_t<T, 1, 8, 8, 4, 2, 1, false, X3>(a, s);
   }
   set_error("unknown block-conv variant");
   return SAD_ERR_ARG;
@@ -735,10 +776,10 @@ bool block_conv_can_pool(const BlockConvArgs& a, int dtype) {
 }
 static bool variant_fits(int v, int cout) {
   if (v == 26) return cout == 64;
-  const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128};
+  const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128, 128};
   if (v == 20 || v == 21) return cout % 64 == 0;
   if (v == 25) return cout == 64;
-  return v >= 9 && v <= 18 && cout % bc[v] == 0;
+  return v >= 9 && v <= 19 && cout % bc[v] == 0;
 }
 
 #if SAD_STAMPS
@@ -827,7 +868,7 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
 #endif
   int rc;
   if (dtype == SAD_BF16X3) {
-    SAD_REQUIRE(v >= 9 && v <= 18, "split-bf16 runs on the implicit-GEMM variants 9..18");
+    SAD_REQUIRE(v >= 9 && v <= 19, "split-bf16 runs on the implicit-GEMM variants 9..19");
     rc = launch_block_v<u16, true>(a, v, s);
   } else {
     rc = dtype == SAD_BF16 ? launch_block_v<u16>(a, v, s) : launch_block_v<float>(a, v, s);

@@ -15,9 +15,10 @@
 //     (sad_frontend_run_windows, frontend.hip): overlapping windows are never
 //     copied, and nothing goes back to the host but one float per window.
 //
-// All of it is HBM / L2 streaming work with a few FMAs per byte (the resampler:
-// K = 2 width + orig taps per output, 459 for 44.1 kHz): plain coalesced
-// kernels, no LDS staging and no MFMA.
+// The mono / window kernels are HBM streaming work; the resampler is fp32-FMA
+// work (K = 2 width + orig taps per output, 459 for 44.1 kHz): register-blocked
+// over frames with the inputs staged in LDS (resample_wide_kernel).  No MFMA:
+// a polyphase FIR is not GEMM-shaped enough to pay for one at fp32.
 #include <math.h>
 
 #include <vector>
@@ -72,6 +73,60 @@ __global__ __launch_bounds__(256) void resample_kernel(const float* __restrict__
       for (int k = k0; k < k1; ++k) acc = fmaf(xp[k], kp[(int64_t)k * nw], acc);
     }
     y[m] = acc;
+  }
+}
+
+// Many phases (nw >= 64: 44.1 / 22.05 kHz -> 32 kHz, nw = 320 / 640, K = 459 /
+// 455): lanes own 64 consecutive phases p, a wave owns RS_R consecutive frames
+// j (RS_R accumulators per lane), and K is walked in chunks of RS_KC taps: the
+// chunk's input samples for the wave's frames are staged in LDS as xs[k][r]
+// (frame-fastest, so one tap's RS_R inputs are 4 broadcast ds_read_b128), the
+// tap's coefficient kt[k][p] is one coalesced load (the table stays in L2), and
+// each tap costs RS_R FMAs per lane.  The sum runs over k in the same order as
+// resample_kernel, so the two give identical results.
+constexpr int RS_R = 16, RS_KC = 64, RS_WAVES = 4;
+__global__ __launch_bounds__(256) void resample_wide_kernel(const float* __restrict__ x, int64_t n_in,
+                                                            const float* __restrict__ kt, int orig, int nw, int width,
+                                                            int K, float* __restrict__ y, int64_t n_out) {
+  __shared__ __attribute__((aligned(16))) float xs[RS_WAVES][RS_KC][RS_R];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int p = blockIdx.y * 64 + lane;
+  const bool pok = p < nw;
+  const int64_t j0 = ((int64_t)blockIdx.x * RS_WAVES + wave) * RS_R;  // this wave's first frame
+  float acc[RS_R];
+#pragma unroll
+  for (int r = 0; r < RS_R; ++r) acc[r] = 0.f;
+  for (int kc = 0; kc < K; kc += RS_KC) {
+    __syncthreads();  // the previous chunk's reads are done
+#pragma unroll 4
+    for (int e = lane; e < RS_KC * RS_R; e += 64) {
+      const int r = e % RS_R, k = e / RS_R;
+      const int64_t i = (j0 + r) * orig + kc + k - width;
+      xs[wave][k][r] = (kc + k < K && i >= 0 && i < n_in) ? x[i] : 0.f;
+    }
+    __syncthreads();
+    const int kn = K - kc < RS_KC ? K - kc : RS_KC;
+    const float* kp = kt + (int64_t)kc * nw + p;
+#pragma unroll 4
+    for (int k = 0; k < kn; ++k) {
+      const float w = pok ? kp[(int64_t)k * nw] : 0.f;
+      const float4* xr = (const float4*)&xs[wave][k][0];
+#pragma unroll
+      for (int q = 0; q < RS_R / 4; ++q) {
+        const float4 v = xr[q];
+        acc[4 * q + 0] = fmaf(v.x, w, acc[4 * q + 0]);
+        acc[4 * q + 1] = fmaf(v.y, w, acc[4 * q + 1]);
+        acc[4 * q + 2] = fmaf(v.z, w, acc[4 * q + 2]);
+        acc[4 * q + 3] = fmaf(v.w, w, acc[4 * q + 3]);
+      }
+    }
+  }
+  if (pok) {
+#pragma unroll
+    for (int r = 0; r < RS_R; ++r) {
+      const int64_t m = (j0 + r) * nw + p;
+      if (m < n_out) y[m] = acc[r];
+    }
   }
 }
 
@@ -207,8 +262,19 @@ extern "C" int sad_resample_run(const sad_resample_plan* p, const float* x, int6
   SAD_REQUIRE(y_len >= n_out, "y_len < the resampled length (sad_resample_out_len)");
   if (y_len == 0) return SAD_OK;
   SAD_REQUIRE(y && (x || n_in == 0), "null pointer");
-  hipLaunchKernelGGL(resample_kernel, dim3(grid_for(y_len)), dim3(256), 0, (hipStream_t)stream, x, n_in, p->d_kt,
-                     p->orig, p->nw, p->width, p->K, y, n_out, y_len);
+  hipStream_t s = (hipStream_t)stream;
+  if (p->nw >= 64 && n_out > 0) {
+    const int64_t frames = (n_out + p->nw - 1) / p->nw;
+    const int64_t gx = (frames + RS_WAVES * RS_R - 1) / (RS_WAVES * RS_R);
+    SAD_REQUIRE(gx < (1ll << 31), "input too long for one launch");
+    hipLaunchKernelGGL(resample_wide_kernel, dim3((unsigned)gx, (unsigned)((p->nw + 63) / 64)), dim3(256), 0, s, x,
+                       n_in, p->d_kt, p->orig, p->nw, p->width, p->K, y, n_out);
+    SAD_CHECK_HIP(hipGetLastError());
+    if (y_len > n_out) SAD_CHECK_HIP(hipMemsetAsync(y + n_out, 0, (size_t)(y_len - n_out) * 4, s));
+    return SAD_OK;
+  }
+  hipLaunchKernelGGL(resample_kernel, dim3(grid_for(y_len)), dim3(256), 0, s, x, n_in, p->d_kt, p->orig, p->nw,
+                     p->width, p->K, y, n_out, y_len);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }

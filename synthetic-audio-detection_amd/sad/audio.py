@@ -43,25 +43,52 @@ def _read_chunks(data: bytes):
     return fmt, payload
 
 
+def _wav_layout(path: str):
+    """RIFF walk over the chunk headers only -> (fmt bytes, data offset, data size)."""
+    fmt = data_off = data_size = None
+    with open(path, 'rb') as f:
+        head = f.read(12)
+        if len(head) < 12 or head[:4] != b'RIFF' or head[8:12] != b'WAVE':
+            raise ValueError('not a RIFF/WAVE file')
+        pos = 12
+        while True:
+            h = f.read(8)
+            if len(h) < 8:
+                break
+            cid, size = h[:4], struct.unpack('<I', h[4:8])[0]
+            if cid == b'fmt ':
+                fmt = f.read(size)
+            elif cid == b'data':
+                data_off, data_size = pos + 8, size
+            pos += 8 + size + (size & 1)
+            f.seek(pos)
+            if fmt is not None and data_off is not None:
+                break
+        end = f.seek(0, 2)
+    if fmt is None or data_off is None:
+        raise ValueError('WAV file lacks fmt/data chunks')
+    return fmt, data_off, min(data_size, end - data_off)
+
+
 def read_wav(path: str):
     """WAV -> (interleaved samples [frames * channels], channels, sample_rate).
-    16-bit PCM stays int16 as stored (the device scales it, sad_pcm_mono_run);
-    every other encoding is decoded to float32 with torchaudio.load's
-    normalize=True scaling."""
-    with open(path, 'rb') as f:
-        data = f.read()
-    fmt, payload = _read_chunks(data)
+    16-bit PCM stays int16 as stored (the device scales it, sad_pcm_mono_run),
+    read straight from the file into one array; every other encoding is
+    decoded to float32 with torchaudio.load's normalize=True scaling."""
+    fmt, off, size = _wav_layout(path)
     tag, ch, sr, _, _, bits = struct.unpack('<HHIIHH', fmt[:16])
     if tag == 0xFFFE and len(fmt) >= 26:  # WAVE_FORMAT_EXTENSIBLE: sub-format GUID's first 2 bytes
         tag = struct.unpack('<H', fmt[24:26])[0]
     width = bits // 8
-    n = len(payload) // (width * ch)
-    raw = payload[:n * width * ch]
+    n = size // (width * ch)
+    if tag == 1 and bits == 16:
+        return np.fromfile(path, '<i2', count=n * ch, offset=off), ch, sr
+    with open(path, 'rb') as f:
+        f.seek(off)
+        raw = f.read(n * width * ch)
     if tag == 1:  # PCM
         if bits == 8:
             x = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128.0) / 128.0
-        elif bits == 16:
-            x = np.frombuffer(raw, '<i2').copy()
         elif bits == 24:
             b = np.frombuffer(raw, np.uint8).reshape(-1, 3).astype(np.int32)
             v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)

@@ -53,12 +53,13 @@ CASES = [
     # a Bottleneck's conv2 (128 channels, no shortcut): halo family, GEMM family
     # (the two sum K in different orders, so they are not compared bitwise)
     ('l2-plain-halo', 3, 32, 128, 128, 1, None, [20, 21]),
-    ('l2-plain-gemm', 3, 32, 128, 128, 1, None, [15, 10, 14]),
-    ('l2-s2', 3, 34, 64, 128, 2, None, [10, 12, 14, 15, 18]),
-    ('l2-ds', 2, 16, 128, 128, 1, 'ds', [10, 12, 14, 15, 18]),
-    ('l3-id', 3, 14, 256, 256, 1, 'id', [13, 17, 10]),
-    ('l3-s2', 2, 18, 128, 256, 2, None, [13, 17]),
-    ('l4-ds', 5, 6, 512, 512, 1, 'ds', [13, 17]),
+    ('l2-plain-gemm', 3, 32, 128, 128, 1, None, [15, 10, 14, 19]),
+    ('l2-s2', 3, 34, 64, 128, 2, None, [10, 12, 14, 15, 18, 19]),
+    ('l2-ds', 2, 16, 128, 128, 1, 'ds', [10, 12, 14, 15, 18, 19]),
+    ('l2-id', 3, 20, 128, 128, 1, 'id', [15, 19]),
+    ('l3-id', 3, 14, 256, 256, 1, 'id', [13, 17, 10, 19]),
+    ('l3-s2', 2, 18, 128, 256, 2, None, [13, 17, 19]),
+    ('l4-ds', 5, 6, 512, 512, 1, 'ds', [13, 17, 19]),
 ]
 
 
