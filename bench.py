@@ -123,6 +123,60 @@ def cpu_baseline(n_clips: int = 64, passes: int = 2):
                       f'files (decode, mono, pad included)'}
 
 
+def ingest_leg(eng, dev, minutes: float = 2.0, reps: int = 3):
+    """SURVEY 8(f) row 1 on the device (sad.ingest, csrc/ingest.hip): one long
+    44.1 kHz stereo int16 recording (synthesised in host memory, as a WAV's data
+    chunk would be read) -> upload -> mono -> resample to 32 kHz -> silence test
+    -> 4 s windows at main()'s overlap 0 read in place by the front end -> the
+    headline engine.  Best of `reps`, HIP events per stage; the resample kernel
+    priced against the fp32 VALU peak (2 K FLOP per output, K = 459 taps)."""
+    import math
+
+    import numpy as np
+    from sad import engine, ingest
+    sr = 44100
+    T = int(minutes * 60 * sr)
+    rs = np.random.RandomState(0)
+    t = np.arange(T) / sr
+    sig = 0.3 * np.sin(2 * np.pi * 440 * t) * (1 + 0.5 * np.sin(2 * np.pi * 0.1 * t)) + 0.05 * rs.randn(T)
+    pcm = np.ascontiguousarray((np.stack([sig, np.roll(sig, 11)]).T * 20000).astype(np.int16)).reshape(-1)
+    fe = engine.FrontEnd(dev)
+    best = None
+    for _ in range(reps + 1):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        ev[0].record()
+        x = torch.from_numpy(pcm).to(dev)
+        ev[1].record()
+        wf = ingest.resampler(sr, 32000, dev)(ingest.mono(x, 2), 128000)
+        ev[2].record()
+        starts, _ = ingest.select_windows(wf, 32000, 4.0, 0.0, 1e-3)
+        w = ingest.Windows(wf, starts, 128000)
+        ev[3].record()
+        eng.forward_maps(fe.windows(wf, w.offsets))
+        ev[4].record()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - h0
+        ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(4)]
+        if best is None or wall < best[0]:
+            best = (wall, ms, len(w), wf.shape[0])
+    wall, ms, nwin, n_out = best
+    K = 2 * math.ceil(6 * 441 / (320 * 0.99)) + 441
+    flop = 2.0 * K * n_out
+    return {'what': f'{minutes:g} min of 44.1 kHz stereo int16 -> device mono + torchaudio sinc resample + '
+                    f'silence test + in-place windows (overlap 0) -> front end + ensemble',
+            'windows': nwin, 'wall_ms': round(wall * 1e3, 3), 'segments_per_s': round(nwin / wall, 1),
+            'h2d_ms': round(ms[0], 3), 'mono_resample_ms': round(ms[1], 3), 'select_ms': round(ms[2], 3),
+            'frontend_ensemble_ms': round(ms[3], 3),
+            'resample_roofline': {'bound': 'fp32 valu', 'taps': K, 'flop': flop,
+                                  'achieved_tflops': round(flop / (ms[1] * 1e-3) / 1e12, 2),
+                                  'peak_tflops': F32_PEAK_TFLOPS,
+                                  'frac_lower_bound': round(flop / (ms[1] * 1e-3) / 1e12 / F32_PEAK_TFLOPS, 4),
+                                  'note': 'timed with the mono kernel, so the fraction is a lower bound on the '
+                                          'resample kernel alone'}}
+
+
 class Mode:
     """One engine configuration timed on this rank's resident PCM."""
 
@@ -355,6 +409,8 @@ def main():
             out['fp32_mode'] = {'value': round(f['value'], 1), 'unit': 'segments/s', 'ms_per_step': round(f['ms'], 3),
                                 'steps': args.fp32_steps, 'peak': F32_PEAK_TFLOPS,
                                 'backbone_tflops': round(BACKBONE_FLOP * B / (f['bb_ms'] * 1e-3) / 1e12, 1)}
+        if world == 1 and not args.kernels_only:
+            out['ingest'] = ingest_leg(head.eng, dev)
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline()
         print(json.dumps(out), flush=True)
