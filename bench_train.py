@@ -3,7 +3,8 @@
 data-parallel step -- device front end (mel norm=None, SpecAugment,
 RandomResizedCrop) + train-mode ResNet-18 forward + CE on pooled features +
 layer4 backward + RCCL all-reduce of the gradients + clip + AdamW -- on 1..8
-MI355X, one process per GPU (torchrun, like bench.py).
+MI355X, one process per GPU: under torchrun, or started bare with --gpus N,
+in which case it starts the N ranks itself (sad/launch.py, like bench.py).
 
 Workload per rank and step: ``--batch-size`` files (default 32, the reference
 default) x 2 segments = 64 segments of synthetic labelled audio
@@ -39,15 +40,22 @@ def main():
     ap.add_argument('--pool', type=int, default=256, help='synthetic training clips per rank')
     ap.add_argument('--eval-clips', type=int, default=64)
     ap.add_argument('--lr', type=float, default=1e-3)
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'], help='gloo: tests only')
+    ap.add_argument('--one-device', action='store_true', help='every rank on cuda:0 (2-rank test on one GPU)')
     args = ap.parse_args()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+    from sad import launch
+    if args.gpus > 1 and not launch.under_launcher():
+        # started bare with --gpus N: N ranks as a torch.distributed.run child (sad/launch.py)
+        sys.exit(launch.relaunch(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    world, rank, local = launch.check_world(args.gpus)
+    dev = torch.device('cuda', 0 if args.one_device else local)
+    torch.cuda.set_device(dev)
     group = None
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
         group = dist.group.WORLD
 
     from sad import augment
@@ -81,7 +89,9 @@ def main():
         idx, t, masks, boxes = next(it)
         waves = torch.cat([wav[idx, :128000], wav[idx, 128000:]], dim=0)
         img = fe(waves, masks, boxes)
-        return tr.train_step(img, t)
+        # every rank takes 2 x batch-size segments: the global batch is known, so
+        # the step needs no all-reduce + host read of it
+        return tr.train_step(img, t, global_batch=img.shape[0] * world)
 
     for _ in range(args.warmup):
         step()

@@ -1,4 +1,4 @@
-"""GPU: the multi-rank branches of bench.py and tools/run_1m.py, run as 2 ranks
+"""GPU: the multi-rank branches of bench.py, bench_train.py and tools/run_1m.py, run as 2 ranks
 on ONE GPU (gloo process group, --one-device; the driver's 8-GPU runs use RCCL
 with one rank per GPU).  Both entry points are started with ``--gpus 2`` and no
 launcher, so they must spawn the 2 ranks themselves (sad/launch.py)."""
@@ -49,3 +49,15 @@ def test_run_1m_two_ranks_matches_one_rank(tmp_path):
     rec, one = run_1m.main(common, return_logits=True)
     assert rec['gathered_rows'] == 1000 and two.shape == one.shape
     assert torch.equal(two, one)
+
+
+def test_bench_train_two_ranks_self_launched():
+    """bench_train.py --gpus 2 without a launcher: 2 ranks, gradient all-reduce
+    over the process group, one JSON line with the whole job's segments."""
+    out = _run(['bench_train.py', '--gpus', '2', '--backend', 'gloo', '--one-device', '--steps', '2', '--warmup', '1',
+                '--batch-size', '4', '--pool', '16', '--eval-clips', '8'])
+    lines = [json.loads(s) for s in out.splitlines() if s.startswith('{')]
+    assert len(lines) == 1, out
+    rec = lines[0]
+    assert rec['n_gpus'] == 2 and rec['config']['parallelism'] == 'dp2'
+    assert rec['segments_per_s'] > 0 and all(l == l for l in rec['train_loss_first_last'])
