@@ -218,3 +218,30 @@ def test_main_long_resampled_file_vs_oracle(tmp_path):
     got = [js['percentages'][k] for k in names]
     assert np.abs(np.array(got) - probs).max() <= 1e-3 * 25, (got, probs)  # |dp| <= |dlogit| / 4
     assert json.load(open(out)) == js
+
+
+@pytest.mark.parametrize('sr,frames', [(44100, 0), (44100, 1), (48000, 3), (32000, 0)])
+def test_preprocess_tiny_files_vs_oracle(tmp_path, sr, frames):
+    """Empty and few-sample files: the resampler's zero-length / shorter-than-
+    the-filter paths, then the zero pad to one window."""
+    import inference_runner as ir
+    from oracle import audio as oaudio
+    x = np.array([[12000, -7000, 300][:frames]] * 2, dtype=np.int64).reshape(2, frames)
+    p = tmp_path / f'tiny_{sr}_{frames}.wav'
+    _write(p, x, sr, 2)
+    wf, _ = ir.preprocess_waveform(str(p), ir.AudioConfig(), DEV)
+    ref, _ = oaudio.preprocess_waveform(str(p))
+    assert wf.shape == ref.shape == (128000,)
+    assert (wf.cpu() - ref).abs().max().item() <= 2e-6
+
+
+def test_main_empty_resampled_file(tmp_path):
+    import inference_runner as ir
+    from conftest import merged_sd
+    mp = tmp_path / 'm.pth'
+    torch.save({'state_dict': merged_sd('n2'), 'metadata': {'class_names': ['A', 'B', 'Real']}}, mp)
+    p = tmp_path / 'empty.wav'
+    _write(p, np.zeros((2, 0), np.int64), 44100, 2)
+    out = tmp_path / 'o.json'
+    js = ir.main(['--merged-model', str(mp), '--audio', str(p), '--output-json', str(out)])
+    assert js == {'filename': str(p), 'segments': [], 'percentages': {}}
