@@ -833,6 +833,35 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   SAD_REQUIRE(a.wt_ld >= a.KH * a.KW * a.Cin + (a.in1 ? a.Cin1 : 0) && (a.wt_ld * ES) % 16 == 0, "weight row length");
   a.wt_bytes = (int64_t)a.Cout * a.wt_ld * ES;
   a.res_bytes = a.res ? (a.M - 1) * a.res_pstride * ES + a.Cout * ES : 0;
+  // The kernels address their operands through 32-bit buffer offsets.  A batch
+  // whose operands exceed that range runs as consecutive launches over image
+  // ranges (every conv here is independent per image, so the results are the
+  // single launch's, bit for bit); the fused-statistics launch, whose
+  // per-workgroup rows would collide, is not split.
+  const int64_t lim = (1ll << 31) - 65536;
+  if ((a.in0_bytes >= lim || a.in1_bytes >= lim || a.res_bytes >= lim) && a.N > 1 &&
+      a.M == (int64_t)a.N * a.Ho * a.Wo && !a.st_part) {
+    const int64_t img0 = (int64_t)a.H * a.W * a.in0_pstride * ES;
+    const int64_t img1 = a.in1 ? (int64_t)a.H1 * a.W1 * a.in1_pstride * ES : 0;
+    const int64_t imgr = a.res ? (int64_t)a.Ho * a.Wo * a.res_pstride * ES : 0;
+    const int64_t imgo = (int64_t)a.Ho * a.Wo * a.out_pstride * ES;
+    const int64_t per = std::max(img0, std::max(img1, imgr));
+    const int64_t nc = (lim - 65536) / per;
+    SAD_REQUIRE(nc >= 1, "one image exceeds the 2 GiB buffer range");
+    for (int64_t n0 = 0; n0 < a.N; n0 += nc) {
+      const int n = (int)std::min<int64_t>(nc, a.N - n0);
+      BlockConvArgs c = a_in;  // logical channel counts (split-bf16 doubles them again)
+      c.N = n;
+      c.M = (int64_t)n * a.Ho * a.Wo;
+      c.in0 = (const char*)a.in0 + n0 * img0;
+      if (a.in1) c.in1 = (const char*)a.in1 + n0 * img1;
+      if (a.res) c.res = (const char*)a.res + n0 * imgr;
+      if (a.out) c.out = (char*)a.out + n0 * imgo;
+      if (a.pool_out) c.pool_out = a.pool_out + n0 * a.Cout;
+      if (int rc = launch_block_conv(c, dtype, s, variant)) return rc;
+    }
+    return SAD_OK;
+  }
   SAD_REQUIRE(a.in0_bytes < (1ll << 31) - 65536 && a.in1_bytes < (1ll << 31) - 65536 && a.wt_bytes < (1ll << 31) &&
                   a.res_bytes < (1ll << 31) - 65536,
               "block conv operand exceeds the 2 GiB buffer range (lower the micro-batch)");

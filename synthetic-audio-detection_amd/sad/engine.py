@@ -274,9 +274,9 @@ class ResNetBackbone:
         self.model_name = model_name
         block, layers, self.num_features = arch_spec(model_name)
         self._dt = _dtype_code(dtype)
-        # the widest activation (layer1 of a Bottleneck net: 128x128x256) must
-        # stay under the kernels' 2 GiB buffer-addressing range
-        self.micro_batch = max(1, min(micro_batch, 128 if dtype == 'bf16' else 64))  # fp32 / bf16x3: 4 B per value
+        # operands past the kernels' 2 GiB buffer range run as several launches
+        # over image ranges (launch_block_conv), so the micro-batch is free
+        self.micro_batch = max(1, micro_batch)
         arrays = _backbone_arrays(base_sd, arch_param_shapes(model_name))
         lay = (_lib.I32 * 4)(*layers)
         self._plan = _lib.P()

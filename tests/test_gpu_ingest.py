@@ -230,6 +230,14 @@ def test_preprocess_tiny_files_vs_oracle(tmp_path, sr, frames):
     p = tmp_path / f'tiny_{sr}_{frames}.wav'
     _write(p, x, sr, 2)
     wf, _ = ir.preprocess_waveform(str(p), ir.AudioConfig(), DEV)
+    if frames == 0 and sr != 32000:
+        # torchaudio's resample views an empty waveform as [-1, 0] and raises, so the
+        # reference's preprocess_waveform fails on such a file; the device path
+        # returns the zero window (and main() then writes the empty-result JSON)
+        with pytest.raises(RuntimeError):
+            oaudio.preprocess_waveform(str(p))
+        assert wf.shape == (128000,) and torch.count_nonzero(wf) == 0
+        return
     ref, _ = oaudio.preprocess_waveform(str(p))
     assert wf.shape == ref.shape == (128000,)
     assert (wf.cpu() - ref).abs().max().item() <= 2e-6
