@@ -274,7 +274,7 @@ def main():
     ap.add_argument('--batch', type=int, default=2048, help='segments per GPU per step')
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'bf16x3', 'fp32'])
     ap.add_argument('--micro-batch', type=int, default=0,
-                    help='segments per backbone launch sequence (0: 512 bf16, 256 bf16x3, 128 fp32); stem/layer1 '
+                    help='segments per backbone launch sequence (0: 1024 bf16, 256 bf16x3, 128 fp32); stem/layer1 '
                          'run in sub-batches of SAD_FRONT_MB=32, layers 2-4 on the whole micro-batch')
     ap.add_argument('--parity-steps', type=int, default=0, help='timed steps of the bf16x3 parity mode '
                                                                 '(0: max(steps // 3, 3); -1: skip)')
@@ -302,7 +302,7 @@ def main():
     from sad import weights as sw
     gold = os.path.join(ROOT, 'tests', 'golden')
     sd = sw.merged_state_dict(0, HEADS, False, bn_stats=sw.load_bn_stats(os.path.join(gold, 'bn_stats_n6.npz')))
-    mbs = {'bf16': 512, 'bf16x3': 256, 'fp32': 128}
+    mbs = {'bf16': 1024, 'bf16x3': 256, 'fp32': 128}
     B = args.batch
     pcm = torch.empty(B, SEG, dtype=torch.int16, device=dev)
     _lib.call('sad_synth_pcm', 0, rank * B, B, SEG, _lib.ptr(pcm), _lib.stream_handle(dev))
@@ -369,7 +369,7 @@ def main():
                        'per_rank_ms_per_step': r['rank_ms_per_step'], 'per_rank_allgather_ms': r['rank_gather_ms']},
             'roofline': {'bound': 'mfma',
                          'kernel': 'sad::block_conv_kernel 256x256 tile (variant 13): the layer3 + layer4 convs, '
-                                   '8 launches per micro-batch of 512, about 35% of the bf16 step',
+                                   '8 launches per micro-batch, about 35% of the bf16 step',
                          'achieved': round(exe, 1), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(exe / peak, 4),
                          'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, '
                                                              + os.path.relpath(TRAFFIC_JSON, ROOT) + ')',
