@@ -163,12 +163,42 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
   // aligned pair loads need an even sample offset for every frame and pair
   const bool pairs = ((hop & 1) == 0) && ((seg_stride & 1) == 0) && ((((uintptr_t)pcm) & (2 * sizeof(IT) - 1)) == 0);
 
+  // int16 path: the next frame's PCM pairs are loaded while this frame is
+  // transformed (software pipeline: a frame's HBM latency no longer stalls its
+  // wave).  The prefetch address is clamped into the segment, so it is always
+  // valid; frames needing reflection (the first / last ones) take the slow path.
+  constexpr bool PREF = sizeof(IT) == 2;
+  uint32_t pre[PREF ? 16 : 1];
+  auto frame_inside = [&](int tt) { return pairs && tt * hop - pad >= 0 && tt * hop - pad + FE_NFFT <= n_samples; };
+  auto prefetch = [&](int tt) __attribute__((always_inline)) {
+    if constexpr (PREF) {
+      int b0 = tt * hop - pad;
+      b0 = b0 < 0 ? 0 : (b0 + FE_NFFT > n_samples ? (n_samples - FE_NFFT) & ~1 : b0);
+      b0 = b0 < 0 ? 0 : b0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = lane + 64 * (q & 3) + 256 * (q >> 2);
+        pre[q] = *(const uint32_t*)(x + b0 + 2 * m);
+      }
+    }
+  };
+  if (PREF && pairs && n_samples >= FE_NFFT) prefetch(f_begin + wave);
+
   for (int t = f_begin + wave; t < f_end; t += FE_WAVES) {
     float2 x16[16];  // z[lane + 64 t'], t' = b + 4 r
     // ---- pass 0 input: z[m] = (y[2m], y[2m+1]) windowed, m = j + 256 r; one
     // 2-sample load per lane (coalesced) where the frame needs no reflection
     const int base = t * hop - pad;
-    const bool inside = pairs && base >= 0 && base + FE_NFFT <= n_samples;
+    const bool inside = frame_inside(t);
+    float2 wvs[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) wvs[q] = *(const float2*)(window + 2 * (lane + 64 * (q & 3) + 256 * (q >> 2)));
+    uint32_t cur[PREF ? 16 : 1];
+    if constexpr (PREF) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) cur[q] = pre[q];
+      if (pairs && n_samples >= FE_NFFT && t + FE_WAVES < f_end) prefetch(t + FE_WAVES);
+    }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int j = lane + 64 * b;
@@ -178,7 +208,7 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
         float e0, e1;
         if (inside) {
           if constexpr (sizeof(IT) == 2) {
-            const uint32_t u = *(const uint32_t*)(x + base + 2 * m);
+            const uint32_t u = cur[b + 4 * r];
             e0 = (float)(short)(u & 0xFFFF);
             e1 = (float)(short)(u >> 16);
           } else {
@@ -195,7 +225,7 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
           e0 = (float)x[i0];
           e1 = (float)x[i1];
         }
-        const float2 wv = *(const float2*)(window + 2 * m);
+        const float2 wv = wvs[b + 4 * r];
         x16[b + 4 * r] = make_float2(e0 * in_scale * wv.x, e1 * in_scale * wv.y);
       }
     }
