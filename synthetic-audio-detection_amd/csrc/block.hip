@@ -725,6 +725,16 @@ static int c128_variant() {
   }();
   return v;
 }
+// SAD_HALO_C128: halo variant for the Cout = 128 stride-1 convs (layer2's second
+// block): 20 (64-channel tiles, two workgroups per tile) or 22 (128-channel
+// tiles, 64 x 64 wave tiles, register epilogue); A/B switch
+static int halo_c128_variant() {
+  static const int v = [] {
+    const char* e = getenv("SAD_HALO_C128");
+    return e ? atoi(e) : 20;
+  }();
+  return v;
+}
 // SAD_X3_RW=0 runs split-bf16 layer1 on the weight-ring halo kernel (variant 20) instead of variant 26 (A/B)
 static bool x3_rw() {
   static const bool v = [] {
@@ -753,7 +763,8 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
     return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   }
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
-  if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo()))) return 20;
+  if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo())))
+    return a.Cout == 128 && !a.res && halo_c128_variant() == 22 ? 22 : 20;
   // small maps (the trainer's 64-segment layer4: M = 16384): 256x256 tiles would
   // leave CUs idle (one workgroup per CU), so split the channel tile (variant
   // 15, 128x256).  Both keep the 256-pixel tile and the same K order, so the
@@ -778,6 +789,7 @@ static bool variant_fits(int v, int cout) {
   if (v == 26) return cout == 64;
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128, 128};
   if (v == 20 || v == 21) return cout % 64 == 0;
+  if (v == 22) return cout % 128 == 0;
   if (v == 25) return cout == 64;
   return v >= 9 && v <= 19 && cout % bc[v] == 0;
 }
@@ -884,8 +896,8 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
     SAD_REQUIRE(halo_ok(a, dtype), "halo conv (variant 25): bf16, 3x3/s1/p1, no GEMM shortcut, H, W % 16");
     return launch_halo_rw(a, s);
   }
-  if (v == 20 || v == 21) {
-    SAD_REQUIRE(halo_ok(a, dtype), "halo conv (variants 20, 21): bf16, 3x3/s1/p1, no GEMM shortcut, H, W % 16");
+  if (v == 20 || v == 21 || v == 22) {
+    SAD_REQUIRE(halo_ok(a, dtype), "halo conv (variants 20-22): bf16, 3x3/s1/p1, no GEMM shortcut, H, W % 16");
     return launch_halo_v(a, v, s);
   }
   SAD_REQUIRE(!a.res || a.res_pstride % 4 == 0, "residual pixel stride must keep 4-channel alignment");

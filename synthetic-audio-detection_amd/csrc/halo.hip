@@ -74,7 +74,11 @@ struct HaloGeo {
   static constexpr int PATCH = NDP * 1024;
   static constexpr int RES = BP * 128;
   static constexpr int WST = BC * 128;
-  static constexpr int NWS = 5;                 // weight ring stages (NWS-1 steps ahead)
+  // channel tiles wider than 64 (variant 22: 128) keep the residual and the
+  // outputs in registers (the X3 epilogue shape; the 128-B staging rows hold
+  // 64 channels) and run a 4-stage weight ring to fit beside the patches
+  static constexpr bool REG = X3 || BC > 64;
+  static constexpr int NWS = BC > 64 ? 4 : 5;   // weight ring stages (NWS-1 steps ahead)
   // patch pieces of the next chunk go out over taps [0, PT) (<= 3 per wave and
   // step), the tile's residual rows over taps [2, 2 + RT)
   static constexpr int PT = QP <= 12 ? 4 : 7;
@@ -82,7 +86,7 @@ struct HaloGeo {
   // X3 (split-bf16): no LDS staging -- the residual comes into registers and
   // the epilogue stores hi/lo straight from them (the staging rows would be
   // 256 B per pixel and not fit beside the ring)
-  static constexpr int OFF_RES = 2 * PATCH, OFF_W = 2 * PATCH + (X3 ? 0 : RES);
+  static constexpr int OFF_RES = 2 * PATCH, OFF_W = 2 * PATCH + (REG ? 0 : RES);
   static constexpr int SMEM = OFF_W + NWS * WST;
   static_assert(TW == 16, "a 16-pixel fragment is one tile row");
   static_assert(BP % TW == 0 && NW % 2 == 0, "tile shape");
@@ -101,6 +105,7 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
   using G = HaloGeo<WC, WP, TC, TP, TW, X3>;
   constexpr int NL = G::NL, BC = G::BC, TH = G::TH, PW = G::PW, PR = G::PR;
   constexpr int QP = G::QP, QR = G::QR, QW = G::QW, NDP = G::NDP, NWS = G::NWS;
+  constexpr bool REG = G::REG;  // register epilogue (X3, or a channel tile > 64)
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
     prep_patch();
   };
   auto res_pieces = [&](int t, int tap) __attribute__((always_inline)) {
-    if constexpr (RES && !X3) {
+    if constexpr (RES && !REG) {
       const __amdgpu_buffer_rsrc_t rr =
           __builtin_amdgcn_make_buffer_rsrc((void*)a.res, (short)0, (int)a.res_bytes, 0x00020000);
       const int b = t / tiles_img, rem = t - b * tiles_img;
@@ -214,21 +219,25 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
   // activation, bf16 -> the tile's LDS staging rows (in place over the
   // residual rows: each lane writes exactly the bytes it read)
   // X3: residual (hi, lo) of the tile in registers, loaded during its last chunk
-  uint2 xres[X3 && RES ? TP : 1][X3 && RES ? TC : 1][2];
+  uint2 xres[REG && RES ? TP : 1][REG && RES ? TC : 1][X3 ? 2 : 1];
   auto x3_pix = [&](int t, int j) __attribute__((always_inline)) {
     const int b = t / tiles_img, rem = t - b * tiles_img;
     const int oy = (rem / tiles_x) * TH + wp * TP + j, ox = (rem % tiles_x) * TW + (lane & 15);
     return (int64_t)(b * a.Ho + oy) * a.Wo + ox;
   };
   auto x3_load_res = [&](int t, int j) __attribute__((always_inline)) {
-    if constexpr (X3 && RES) {
+    if constexpr (REG && RES) {
       const u16* rp = (const u16*)a.res + x3_pix(t, j) * a.res_pstride;
 #pragma unroll
       for (int i = 0; i < TC; ++i) {
         const int co = c0 + wc * 16 * TC + i * 16 + (lane >> 4) * 4;
-        const int pc = ((co >> 5) << 6) + (co & 31);
-        xres[j][i][0] = *(const uint2*)(rp + pc);
-        xres[j][i][1] = *(const uint2*)(rp + pc + 32);
+        if constexpr (X3) {
+          const int pc = ((co >> 5) << 6) + (co & 31);
+          xres[j][i][0] = *(const uint2*)(rp + pc);
+          xres[j][i][X3 ? 1 : 0] = *(const uint2*)(rp + pc + 32);
+        } else {
+          xres[j][i][0] = *(const uint2*)(rp + co);
+        }
       }
     }
   };
@@ -241,18 +250,38 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
         const int co = c0 + wc * 16 * TC + i * 16 + (lane >> 4) * 4;
         const int pc = ((co >> 5) << 6) + (co & 31);
         float v[4];
+        if constexpr (X3) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[i][r];
-        if constexpr (RES) {
-          const uint2 h = xres[j][i][0], l = xres[j][i][1];
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[i][r];
+        } else {  // variant 22: the bias is re-read here (L1) instead of held in 16 VGPRs
+          const float4 bb = *(const float4*)(a.bias + co);
+          v[0] = acc[i][j][0] + bb.x;
+          v[1] = acc[i][j][1] + bb.y;
+          v[2] = acc[i][j][2] + bb.z;
+          v[3] = acc[i][j][3] + bb.w;
+        }
+        if constexpr (RES && X3) {
+          const uint2 h = xres[j][i][0], l = xres[j][i][X3 ? 1 : 0];
           v[0] += __uint_as_float(h.x << 16) + __uint_as_float(l.x << 16);
           v[1] += __uint_as_float(h.x & 0xFFFF0000u) + __uint_as_float(l.x & 0xFFFF0000u);
           v[2] += __uint_as_float(h.y << 16) + __uint_as_float(l.y << 16);
           v[3] += __uint_as_float(h.y & 0xFFFF0000u) + __uint_as_float(l.y & 0xFFFF0000u);
+        } else if constexpr (RES) {
+          const uint2 h = xres[j][i][0];
+          v[0] += __uint_as_float(h.x << 16);
+          v[1] += __uint_as_float(h.x & 0xFFFF0000u);
+          v[2] += __uint_as_float(h.y << 16);
+          v[3] += __uint_as_float(h.y & 0xFFFF0000u);
         }
         if constexpr (RELU)
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        if constexpr (!X3) {  // plain bf16 (variant 22): one 8-B store per lane
+          *(uint2*)(op + co) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                          (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
         u16 hh[4], ll[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -412,13 +441,13 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
       constexpr int tap = decltype(tap_c)::value;
       if (!(ab & 2)) {
         if (wloader) {
-          // w(g) was issued at step g-4; younger: w(g+1..g+3) (weight waves store nothing)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * QW) : "memory");
+          // w(g) was issued at step g-(NWS-1); younger: w(g+1..g+NWS-2) (weight waves store nothing)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NWS - 2) * QW) : "memory");
         } else if (tap == 0) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next chunk's patch + this tile's residual
         }
       }
-      if constexpr (tap == 1 && !X3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging rows written
+      if constexpr (tap == 1 && !REG) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging rows written
       if (!(ab & 4)) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (!(ab & 1)) {
@@ -432,17 +461,17 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
                 dma16_m0(r0, poff[k], lds0 + (pbuf ^ 1) * G::PATCH + (lw + NL * k) * 1024);
             if constexpr (tap == G::PT - 1) advance_patch();
           }
-          if constexpr (tap == 1 && !X3)
+          if constexpr (tap == 1 && !REG)
             if (after_tile) store_tile(t - 1);
           if constexpr (RES && tap >= 2 && tap < 2 + G::RT)
             if (last_chunk) res_pieces(t, tap);
         }
       }
-      if constexpr (X3 && RES && tap >= 2 && tap < 2 + TP)
+      if constexpr (REG && RES && tap >= 2 && tap < 2 + TP)
         if (last_chunk) x3_load_res(t, tap - 2);
       if constexpr (tap == 0)
         if (after_tile && !(ab & 8)) {
-          if constexpr (X3)
+          if constexpr (REG)
             x3_epilogue(t - 1);
           else
             epilogue();
@@ -460,7 +489,7 @@ __global__ __launch_bounds__(64 * WC * WP, WC * WP / 4) void halo_conv_kernel(Bl
   for (int c = 0; c < nchunks; ++c) chunk();
   // last tile: its residual rows were issued in its last chunk; publish, then store
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (X3) {
+  if constexpr (REG) {
     x3_epilogue(tp_end - 1);
     return;
   }
@@ -1046,6 +1075,8 @@ static int launch_halo_g(const BlockConvArgs& a, hipStream_t s) {
 // Variants (channels x tile (TH x TW), waves, wave tile, LDS; one WG per CU):
 //  20: 64 x 16x16  8w  64x32  154 KB
 //  21: 64 x 16x16  4w  64x64  156 KB (one wave per SIMD: half the LDS fragment reads per MFMA)
+//  22: 128 x 16x16 8w  64x64  146 KB (Cout 128: one patch read per tile instead of two, a
+//      third fewer LDS fragment reads per MFMA than 20; 4-stage weight ring, register epilogue)
 int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s, bool x3) {
   if (x3) {
     SAD_REQUIRE(v == 20, "split-bf16 halo conv: variant 20");
@@ -1059,6 +1090,7 @@ int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s, bool x3) {
   switch (v) {
     case 20: return launch_halo_g<1, 8, 4, 2, 16>(a, s);
     case 21: return launch_halo_g<1, 4, 4, 4, 16>(a, s);
+    case 22: return launch_halo_g<2, 4, 4, 4, 16>(a, s);
   }
   set_error("unknown halo-conv variant");
   return SAD_ERR_ARG;

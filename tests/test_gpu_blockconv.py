@@ -49,10 +49,11 @@ def _check(out, ref):
 CASES = [
     ('l1-res', 5, 128, 64, 64, 1, 'res', [20, 21, 25]),  # 320 tiles: 2 per workgroup on some
     ('l1-plain', 2, 48, 64, 64, 1, None, [9, 11, 16, 20, 25]),
-    ('l2-res', 2, 32, 128, 128, 1, 'res', [20, 21]),
+    ('l2-res', 2, 32, 128, 128, 1, 'res', [20, 21, 22]),
     # a Bottleneck's conv2 (128 channels, no shortcut): halo family, GEMM family
     # (the two sum K in different orders, so they are not compared bitwise)
-    ('l2-plain-halo', 3, 32, 128, 128, 1, None, [20, 21]),
+    ('l2-plain-halo', 3, 32, 128, 128, 1, None, [20, 21, 22]),
+    ('l2-plain-halo-256', 2, 32, 128, 256, 1, None, [20, 22]),
     ('l2-plain-gemm', 3, 32, 128, 128, 1, None, [15, 10, 14, 19]),
     ('l2-s2', 3, 34, 64, 128, 2, None, [10, 12, 14, 15, 18, 19]),
     ('l2-ds', 2, 16, 128, 128, 1, 'ds', [10, 12, 14, 15, 18, 19]),
