@@ -32,6 +32,7 @@
 //    store, so the weight waves' counted waits see DMAs only.
 //  * operands swapped (C = W . X^T): each lane holds 4 consecutive output
 //    channels of one pixel.
+#include <type_traits>
 #include <utility>
 
 #include "common.hpp"
@@ -601,15 +602,19 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
   const int fr = lane & 15, fg = lane >> 4;
   StatLane<ST ? TC : 1> stat;
   stat.zero();
-  // lane's pixel of fragment j: tile row 2wp + j, column fr; channels i*16 + fg*4 .. +3
-  auto pix_index = [&](int t, int j) __attribute__((always_inline)) {
+  // lane's pixel of fragment j: tile row 2wp + j, column fr; channels i*16 + fg*4 .. +3.
+  // The tile's first pixel is wave-uniform (64-bit scalar math); the lane's
+  // offset from it is a 32-bit VGPR product, so the per-j addresses cost no
+  // 64-bit vector multiplies
+  auto tile_pix = [&](int t) __attribute__((always_inline)) {
     const int b = t / tiles_img, rem = t - b * tiles_img;
-    const int oy = (rem / tiles_x) * TH + 2 * wp + j, ox = (rem % tiles_x) * TW + fr;
-    return (int64_t)(b * a.Ho + oy) * a.Wo + ox;
+    const int oy0 = (rem / tiles_x) * TH, ox0 = (rem % tiles_x) * TW;
+    return (int64_t)(b * a.Ho + oy0) * a.Wo + ox0;
   };
+  auto lane_pix = [&](int j) __attribute__((always_inline)) { return (2 * wp + j) * a.Wo + fr; };
   auto load_res = [&](int t, int j) __attribute__((always_inline)) {
     if constexpr (RES) {
-      const u16* rp = (const u16*)a.res + pix_index(t, j) * a.res_pstride + fg * 4;
+      const u16* rp = (const u16*)a.res + tile_pix(t) * a.res_pstride + (lane_pix(j) * (int)a.res_pstride + fg * 4);
 #pragma unroll
       for (int i = 0; i < TC; ++i) resv[i][j] = *(const uint2*)(rp + i * 16);
     }
@@ -625,7 +630,7 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < TP; ++j) {
-      u16* op = (u16*)a.out + pix_index(t, j) * a.out_pstride + fg * 4;
+      u16* op = (u16*)a.out + tile_pix(t) * a.out_pstride + (lane_pix(j) * (int)a.out_pstride + fg * 4);
 #pragma unroll
       for (int i = 0; i < TC; ++i) {
         float v[4];
@@ -643,8 +648,7 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
         uint2 q;
         q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
         q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *(uint2*)(op + i * 16) = q;
-        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        *(uint2*)(op + i * 16) = q;  // (tap 0 of the next tile restarts acc from zero)
       }
     }
   };
@@ -669,13 +673,25 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
       }
     }
   };
-  auto mma_tap = [&](const uint4 (&wf)[2][TC], const uint4 (&pf)[2][TP]) __attribute__((always_inline)) {
+  // tap 0's first K-half starts each accumulator from an inline zero (no
+  // per-tile v_mov zeroing of the 32 accumulator registers)
+  auto mma_tap = [&](const uint4 (&wf)[2][TC], const uint4 (&pf)[2][TP], auto first) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < TC; ++i)
 #pragma unroll
-        for (int j = 0; j < TP; ++j) mfma_chunk<u16>(wf[s][i], pf[s][j], acc[i][j]);
+        for (int j = 0; j < TP; ++j) {
+          if constexpr (decltype(first)::value) {
+            if (s == 0) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[0][i]),
+                                                                  __builtin_bit_cast(bf16x8, pf[0][j]),
+                                                                  f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+              continue;
+            }
+          }
+          mfma_chunk<u16>(wf[s][i], pf[s][j], acc[i][j]);
+        }
   };
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -697,7 +713,7 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (k < 8) {
         read_tap(wf[(k + 1) & 1], pf[(k + 1) & 1], k + 1, pb);
-        mma_tap(wf[k & 1], pf[k & 1]);
+        mma_tap(wf[k & 1], pf[k & 1], std::integral_constant<bool, k == 0>{});
         // the next tap's 12 reads spread over this tap's 16 MFMAs
 #pragma unroll
         for (int q = 0; q < 2 * (TC + TP); ++q) {
@@ -706,7 +722,7 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
         }
         __builtin_amdgcn_sched_group_barrier(0x008, 2 * TC * TP - 2 * (TC + TP), 0);
       } else {
-        mma_tap(wf[k & 1], pf[k & 1]);
+        mma_tap(wf[k & 1], pf[k & 1], std::integral_constant<bool, false>{});
       }
     });
     __builtin_amdgcn_sched_barrier(0);
