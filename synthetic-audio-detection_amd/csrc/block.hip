@@ -815,8 +815,8 @@ static int stamp_report(const BlockConvArgs& a, hipStream_t s) {
       ++n;
     }
     if (n)
-      fprintf(stderr, "stamps M=%lld Cout=%d K=%d wave %d: %d steps, cycles/step wait+barrier %.0f | reads+dma %.0f | "
-              "mfma issue %.0f | tail %.0f | total %.0f\n", (long long)a.M, a.Cout, a.KH * a.KW * a.Cin, w, n,
+      fprintf(stderr, "stamps M=%lld Cout=%d K=%d wave %d: %d steps, cycles/step phases 0-1 %.0f | 1-2 %.0f | "
+              "2-3 %.0f | 3-next %.0f | total %.0f\n", (long long)a.M, a.Cout, a.KH * a.KW * a.Cin, w, n,
               ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, (ph[0] + ph[1] + ph[2] + ph[3]) / n);
   }
   return SAD_OK;
@@ -894,7 +894,16 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   }
   if (v == 25) {
     SAD_REQUIRE(halo_ok(a, dtype), "halo conv (variant 25): bf16, 3x3/s1/p1, no GEMM shortcut, H, W % 16");
+#if SAD_STAMPS
+    static uint64_t* stamp_buf25 = nullptr;
+    if (!stamp_buf25) SAD_CHECK_HIP(hipMalloc(&stamp_buf25, 2 * 4096 * 8));
+    SAD_CHECK_HIP(hipMemsetAsync(stamp_buf25, 0, 2 * 4096 * 8, s));
+    a.stamps = stamp_buf25;
+    const int rc25 = launch_halo_rw(a, s);
+    return rc25 == SAD_OK ? stamp_report(a, s) : rc25;
+#else
     return launch_halo_rw(a, s);
+#endif
   }
   if (v == 20 || v == 21 || v == 22) {
     SAD_REQUIRE(halo_ok(a, dtype), "halo conv (variants 20-22): bf16, 3x3/s1/p1, no GEMM shortcut, H, W % 16");

@@ -39,6 +39,10 @@
 #include "igemm.hpp"
 #include "kernels.hpp"
 
+#ifndef SAD_STAMPS
+#define SAD_STAMPS 0
+#endif
+
 namespace sad {
 
 // f(std::integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time
@@ -699,8 +703,23 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
 
   uint4 wf[2][2][TC], pf[2][2][TP];
   int pb = 0;
+  // diagnostic build (-DSAD_STAMPS=1): s_memtime of waves 0 and 4 of workgroup 0
+  // per tile -- 0 tile start, 1 taps issued, 2 before the tile barrier, 3 after it
+  const bool stamp_on = SAD_STAMPS && a.stamps && blockIdx.x == 0 && (wave == 0 || wave == 4);
+  auto stamp = [&](int g, int slot) __attribute__((always_inline)) {
+    if constexpr (SAD_STAMPS) {
+      if (stamp_on && g < 1024) {
+        __builtin_amdgcn_sched_barrier(0);
+        uint64_t t_;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (lane == 0) a.stamps[(size_t)(wave == 0 ? 0 : 1) * 4096 + (size_t)g * 4 + slot] = t_;
+      }
+    }
+  };
   for (int t = tp_begin; t < tp_end; ++t) {
     const bool has_next = t + 1 < tp_end;
+    stamp(t - tp_begin, 0);
     read_tap(wf[0], pf[0], 0, pb);
     static_for<9>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
@@ -726,6 +745,7 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
       }
     });
     __builtin_amdgcn_sched_barrier(0);
+    stamp(t - tp_begin, 1);
     if (has_next) prep_patch(t + 2 < tp_end ? t + 2 : t + 1);
     // early waves: epilogue, then wait for their DMAs/loads (the stores, youngest, may stay in flight)
     if (early) {
@@ -734,8 +754,10 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    stamp(t - tp_begin, 2);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    stamp(t - tp_begin, 3);
     if (!early) epilogue(t);
     pb ^= 1;
   }
