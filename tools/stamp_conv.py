@@ -30,15 +30,18 @@ def rnd(shape, seed, scale=1.0):
 
 
 def main():
-    x = rnd((32, 128, 128, 64), 1)
-    res = rnd((32, 128, 128, 64), 2)
+    # the bench's Infinity-Cache-sized sub-batch (32 images: 8 tiles per workgroup)
+    # and 512 images (128 tiles per workgroup, operands from HBM)
     w = rnd((64, 576), 3, (2 / 576) ** 0.5)
     b = torch.zeros(64, device=DEV)
-    for name, kw in (('layer1 conv (v25)', {}), ('layer1 conv + res (v25)', {'res': res})):
-        for it in range(3):
-            print(f'--- {name} iteration {it}', file=sys.stderr, flush=True)
-            block_conv(x, w, b, 1, 1, variant=25, **kw)
-            torch.cuda.synchronize()
+    for n in (32, 512):
+        x = rnd((n, 128, 128, 64), 1)
+        res = rnd((n, 128, 128, 64), 2)
+        for name, kw in (('layer1 conv (v25)', {}), ('layer1 conv + res (v25)', {'res': res})):
+            for it in range(3):
+                print(f'--- {name}, {n} images, iteration {it}', file=sys.stderr, flush=True)
+                block_conv(x, w, b, 1, 1, variant=25, **kw)
+                torch.cuda.synchronize()
     x4 = rnd((256, 16, 16, 512), 4)
     w4 = rnd((512, 4608), 5, (2 / 4608) ** 0.5)
     b4 = torch.zeros(512, device=DEV)
