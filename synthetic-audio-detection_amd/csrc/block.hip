@@ -692,7 +692,6 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
 
 int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s, bool x3 = false);
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s);
-int launch_halo_rw2(const BlockConvArgs& a, hipStream_t s);
 int launch_halo_rw_x3(const BlockConvArgs& a, hipStream_t s);
 
 // halo kernel (variant 20): bf16 stride-1 3x3 with Cout <= 128 (layer1, layer2's
@@ -736,15 +735,6 @@ static int halo_c128_variant() {
   }();
   return v;
 }
-// SAD_L1_VARIANT: layer1's resident-weight kernel, 25 (staggered epilogue) or
-// 27 (epilogue pipelined into the next tile's taps); A/B switch
-static int l1_variant() {
-  static const int v = [] {
-    const char* e = getenv("SAD_L1_VARIANT");
-    return e ? atoi(e) : 25;
-  }();
-  return v;
-}
 // SAD_X3_RW=0 runs split-bf16 layer1 on the weight-ring halo kernel (variant 20) instead of variant 26 (A/B)
 static bool x3_rw() {
   static const bool v = [] {
@@ -772,8 +762,7 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
     if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64 && x3_rw()) return 26;
     return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   }
-  if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64)  // layer1: resident weights
-    return !a.st_part && l1_variant() == 27 ? 27 : 25;
+  if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
   if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo())))
     return a.Cout == 128 && !a.res && halo_c128_variant() == 22 ? 22 : 20;
   // small maps (the trainer's 64-segment layer4: M = 16384): 256x256 tiles would
@@ -801,7 +790,7 @@ static bool variant_fits(int v, int cout) {
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128, 128};
   if (v == 20 || v == 21) return cout % 64 == 0;
   if (v == 22) return cout % 128 == 0;
-  if (v == 25 || v == 27) return cout == 64;
+  if (v == 25) return cout == 64;
   return v >= 9 && v <= 19 && cout % bc[v] == 0;
 }
 
@@ -915,11 +904,6 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
 #else
     return launch_halo_rw(a, s);
 #endif
-  }
-  if (v == 27) {
-    SAD_REQUIRE(halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64,
-                "halo conv (variant 27): bf16, 3x3/s1/p1, Cin = Cout = 64, no GEMM shortcut, H, W % 16");
-    return launch_halo_rw2(a, s);
   }
   if (v == 20 || v == 21 || v == 22) {
     SAD_REQUIRE(halo_ok(a, dtype), "halo conv (variants 20-22): bf16, 3x3/s1/p1, no GEMM shortcut, H, W % 16");

@@ -798,270 +798,6 @@ static int launch_halo_rw_t(const BlockConvArgs& a, hipStream_t s) {
   return SAD_OK;
 }
 
-// ---------------------------------------------------------------------------
-// Variant 27: variant 25 with the epilogue software-pipelined into the next
-// tile's taps.  In-kernel stamps of variant 25 (tools/stamp_conv.py; 32-image
-// sub-batch) put a tile at ~8,000 cycles for 4,608 cycles of MFMA per SIMD: the
-// staggered epilogue leaves one wave per SIMD computing for long stretches
-// (wave 1: late epilogue 1.5k, taps 5.3k; wave 0: epilogue + wait 2.1k,
-// barrier 1.9k), so LDS latency goes unhidden.  Here every wave keeps two
-// accumulator sets: tile t's MFMAs go to one while tile t-1's epilogue (bias
-// [+ residual] + ReLU + one 8-B store per (i, j) pair) runs as one pair per
-// two pairs per tap between the MFMAs of taps 5..8 -- after the tile's patch
-// DMA pieces, so the stores are the youngest memory operations at the tile-end
-// wait -- no epilogue phase, no stagger.  A residual pair is loaded three taps
-// before its use; the bias is re-read (L1) rather than held.
-template <bool RES, bool RELU>
-__global__ __launch_bounds__(512, 1) void halo_rw2_kernel(BlockConvArgs a) {
-  constexpr int NW = 8, TC = 4, TP = 2, TW = 16, TH = 16;
-  constexpr int PW = TW + 2, PR = PW * (TH + 2);  // 18 x 18 patch rows
-  constexpr int NDP = (PR + 7) / 8;               // 41 DMA pieces per patch
-  constexpr int QP = (NDP + NW - 1) / NW;         // <= 6 per wave
-  constexpr int WBYTES = 9 * 64 * 128;            // resident weights
-  constexpr int PATCH = NDP * 1024;
-  constexpr int NPAIR = TC * TP;                  // epilogue pairs, one per tap 0..7
-  static_assert(NPAIR == 8, "one epilogue pair per tap 0..7");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wp = wave;  // tile rows 2wp, 2wp+1; all 64 channels
-  const int w = xcd_remap(blockIdx.x, gridDim.x);
-  const int tiles_x = a.W / TW, tiles_img = tiles_x * (a.H / TH);
-  const int tiles_p = a.N * tiles_img;
-  const int tp_begin = (int)((int64_t)w * tiles_p / gridDim.x), tp_end = (int)((int64_t)(w + 1) * tiles_p / gridDim.x);
-  if (tp_begin >= tp_end) return;
-
-  const __amdgpu_buffer_rsrc_t r0 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, (int)a.wt_bytes, 0x00020000);
-  const int ps0 = (int)a.in0_pstride * 2;
-  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-
-  int poff[QP];
-  auto prep_patch = [&](int pt) __attribute__((always_inline)) {
-    const int b = pt / tiles_img, rem = pt - b * tiles_img;
-    const int oy0 = (rem / tiles_x) * TH, ox0 = (rem % tiles_x) * TW;
-#pragma unroll
-    for (int k = 0; k < QP; ++k) {
-      const int pr = 8 * (wave + NW * k) + (lane >> 3);
-      const int py = pr / PW, px = pr - py * PW;
-      const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
-      poff[k] = (pr < PR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
-                    ? ((b * a.H + iy) * a.W + ix) * ps0 + ((lane & 7) ^ (pr & 6)) * 16
-                    : 0x7FFFFFF0;
-    }
-  };
-  auto patch_piece = [&](int k, int pb) __attribute__((always_inline)) {
-    if (NDP % NW == 0 || wave + NW * k < NDP)
-      dma16_m0(r0, poff[k], lds0 + WBYTES + pb * PATCH + (wave + NW * k) * 1024);
-  };
-
-  // prologue: resident weights (72 pieces, 9 per wave) + the first patch
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int q = wave + NW * i;
-    const int tap = q >> 3, co = 8 * (q & 7) + (lane >> 3);
-    dma16_m0(rw, co * (a.wt_ld * 2) + tap * 128 + ((lane & 7) ^ (co & 6)) * 16, lds0 + tap * 8192 + (q & 7) * 1024);
-  }
-  prep_patch(tp_begin);
-#pragma unroll
-  for (int k = 0; k < QP; ++k) patch_piece(k, 0);
-  if (tp_begin + 1 < tp_end) prep_patch(tp_begin + 1);
-
-  const int fr = lane & 15, fg = lane >> 4;
-  // the tile's first pixel (wave-uniform) and the lane's offset from it
-  auto tile_pix = [&](int t) __attribute__((always_inline)) {
-    const int b = t / tiles_img, rem = t - b * tiles_img;
-    return (int64_t)(b * a.Ho + (rem / tiles_x) * TH) * a.Wo + (rem % tiles_x) * TW;
-  };
-  auto lane_pix = [&](int j) __attribute__((always_inline)) { return (2 * wp + j) * a.Wo + fr; };
-
-  // lfr: the lane's fragment row, re-materialised per tile (an empty asm makes
-  // it opaque) so the per-tap LDS addresses are not hoisted out of the tile
-  // loop into dozens of live registers
-  auto read_tap = [&](uint4 (&wf)[2][TC], uint4 (&pf)[2][TP], int k, int pb, int lfr) __attribute__((always_inline)) {
-    const char* wb = smem + k * 8192;
-    const char* pbuf = smem + WBYTES + pb * PATCH;
-    const int ky = k / 3, kx = k - ky * 3;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = (lfr >> 4 & 0) + fg + 4 * s;
-#pragma unroll
-      for (int i = 0; i < TC; ++i) {
-        const int r = i * 16 + lfr;
-        wf[s][i] = *(const uint4*)(wb + r * 128 + (hswz(r, c) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < TP; ++j) {
-        const int r = (2 * wp + j + ky) * PW + kx + lfr;
-        pf[s][j] = *(const uint4*)(pbuf + r * 128 + (hswz(r, c) << 4));
-      }
-    }
-  };
-
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  f32x4 accA[TC][TP], accB[TC][TP];
-  uint2 rv[RES ? NPAIR : 1];  // residual pairs in flight
-  uint4 wf[2][2][TC], pf[2][2][TP];
-  int pb = 0;
-
-  auto load_res = [&](int tt, int q) __attribute__((always_inline)) {
-    if constexpr (RES) {
-      const int i = q / TP, j = q % TP;
-      const u16* rp = (const u16*)a.res + tile_pix(tt) * a.res_pstride +
-                      (lane_pix(j) * (int)a.res_pstride + fg * 4 + i * 16);
-      rv[RES ? q : 0] = *(const uint2*)rp;
-    }
-  };
-  // one epilogue pair q = (i, j) of tile tp: bias [+ residual], ReLU, 8-B store
-  auto epi_pair = [&](int tp, int q, const f32x4 (&prev)[TC][TP]) __attribute__((always_inline)) {
-    const int i = q / TP, j = q % TP;
-    const float4 bb = *(const float4*)(a.bias + i * 16 + fg * 4);
-    u16* op = (u16*)a.out + tile_pix(tp) * a.out_pstride + (lane_pix(j) * (int)a.out_pstride + fg * 4 + i * 16);
-    float v[4] = {prev[i][j][0] + bb.x, prev[i][j][1] + bb.y, prev[i][j][2] + bb.z, prev[i][j][3] + bb.w};
-    if constexpr (RES) {
-      const uint2 r2 = rv[RES ? q : 0];
-      v[0] += __uint_as_float(r2.x << 16);
-      v[1] += __uint_as_float(r2.x & 0xFFFF0000u);
-      v[2] += __uint_as_float(r2.y << 16);
-      v[3] += __uint_as_float(r2.y & 0xFFFF0000u);
-    }
-    if constexpr (RELU)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-    *(uint2*)op = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
-                             (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
-  };
-
-  // tile t into `acc`; tile t-1's epilogue from `prev`, pairs 2m, 2m+1 at tap 5 + m
-  auto tile_body = [&](int t, f32x4 (&acc)[TC][TP], const f32x4 (&prev)[TC][TP], auto hp)
-                       __attribute__((always_inline)) {
-    constexpr bool has_prev = decltype(hp)::value;  // compile-time: no branches inside the taps
-    const bool has_next = t + 1 < tp_end;
-    int lfr = fr;
-    asm volatile("" : "+v"(lfr));
-    read_tap(wf[0], pf[0], 0, pb, lfr);
-    static_for<9>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int k = decltype(kc)::value;
-      __builtin_amdgcn_sched_barrier(0);
-      // VMEM order within a tile: patch pieces (taps 0..5), residual loads
-      // (taps 2..5), then the stores (taps 5..8) -- the stores are the youngest
-      // at the tile-end wait, so it never waits for a store to complete
-      if constexpr (k < QP)
-        if (has_next) patch_piece(k, pb ^ 1);
-      if constexpr (has_prev && k >= 2 && k <= 5) {
-        load_res(t - 1, 2 * (k - 2));  // used three taps later
-        load_res(t - 1, 2 * (k - 2) + 1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // the epilogue pairs of taps 5..8 are scheduled between the MFMAs below
-      if constexpr (has_prev && k >= 5) {
-        epi_pair(t - 1, 2 * (k - 5), prev);
-        epi_pair(t - 1, 2 * (k - 5) + 1, prev);
-      }
-      constexpr int cur = k & 1;
-      if constexpr (k < 8) read_tap(wf[cur ^ 1], pf[cur ^ 1], k + 1, pb, lfr);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int i = 0; i < TC; ++i)
-#pragma unroll
-          for (int j = 0; j < TP; ++j) {
-            if (k == 0 && s2 == 0)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[0][0][i]),
-                                                                  __builtin_bit_cast(bf16x8, pf[0][0][j]),
-                                                                  f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            else
-              mfma_chunk<u16>(wf[cur][s2][i], pf[cur][s2][j], acc[i][j]);
-          }
-      if constexpr (k < 8) {
-        // the next tap's 12 reads spread over this tap's 16 MFMAs (+ the
-        // epilogue's VALU, 3 per MFMA gap, on taps 5..8)
-#pragma unroll
-        for (int q = 0; q < 2 * (TC + TP); ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          if constexpr (has_prev && k >= 5) __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * TC * TP - 2 * (TC + TP), 0);
-      } else if constexpr (has_prev) {
-#pragma unroll
-        for (int q = 0; q < 2 * TC * TP; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-        }
-      }
-    });
-    __builtin_amdgcn_sched_barrier(0);
-    if (has_next) prep_patch(t + 2 < tp_end ? t + 2 : t + 1);
-    // the next tile's patch pieces must have landed; the previous tile's 8
-    // epilogue stores (the youngest) may stay in flight
-    if constexpr (has_prev)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPAIR) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    pb ^= 1;
-  };
-  using F = std::integral_constant<bool, false>;
-  using T = std::integral_constant<bool, true>;
-  tile_body(tp_begin, accA, accB, F{});  // the first tile: no epilogue to pipeline
-  int t = tp_begin + 1;
-  for (; t + 1 < tp_end; t += 2) {
-    tile_body(t, accB, accA, T{});
-    tile_body(t + 1, accA, accB, T{});
-  }
-  const bool odd = t < tp_end;  // one tile left (into B); else the last tile is in A
-  if (odd) tile_body(t, accB, accA, T{});
-  // the last tile's epilogue
-#pragma unroll
-  for (int q = 0; q < NPAIR; ++q) load_res(tp_end - 1, q);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int q = 0; q < NPAIR; ++q) {
-    if (odd)
-      epi_pair(tp_end - 1, q, accB);
-    else
-      epi_pair(tp_end - 1, q, accA);
-  }
-}
-
-template <bool RES, bool RELU>
-static int launch_halo_rw2_t(const BlockConvArgs& a, hipStream_t s) {
-  constexpr int smem = 9 * 64 * 128 + 2 * 41 * 1024;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)halo_rw2_kernel<RES, RELU>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              smem);
-    attr = true;
-  }
-  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.in1,
-              "halo conv: 3x3, stride 1, pad 1, no GEMM shortcut");
-  SAD_REQUIRE(a.Cin == 64 && a.Cout == 64, "resident-weight halo conv (variant 27): Cin = Cout = 64");
-  SAD_REQUIRE(a.W % 16 == 0 && a.H % 16 == 0 && a.Ho == a.H && a.Wo == a.W, "image must tile exactly");
-  SAD_REQUIRE(a.wt_ld >= 9 * a.Cin && (a.wt_ld * 2) % 16 == 0, "weight row length");
-  SAD_REQUIRE(!a.res || a.res_pstride >= a.Cout, "residual pixel stride");
-  SAD_REQUIRE(a.out_pstride % 4 == 0 && (!a.res || a.res_pstride % 4 == 0), "8-B aligned pixel rows");
-  SAD_REQUIRE(!a.st_part, "variant 27 has no fused statistics (variant 25 does)");
-  const int64_t tiles_p = (int64_t)a.N * (a.H / 16) * (a.W / 16);
-  SAD_REQUIRE(tiles_p < (1ll << 31) && (int64_t)a.N * a.H * a.W * a.in0_pstride * 2 < (1ll << 31),
-              "too large for one launch");
-  const int64_t g = std::min<int64_t>(tiles_p, 256);
-  hipLaunchKernelGGL((halo_rw2_kernel<RES, RELU>), dim3((unsigned)g), dim3(512), smem, s, a);
-  SAD_CHECK_HIP(hipGetLastError());
-  return SAD_OK;
-}
-
-int launch_halo_rw2(const BlockConvArgs& a, hipStream_t s) {
-  if (a.res) return a.relu ? launch_halo_rw2_t<true, true>(a, s) : launch_halo_rw2_t<true, false>(a, s);
-  return a.relu ? launch_halo_rw2_t<false, true>(a, s) : launch_halo_rw2_t<false, false>(a, s);
-}
-
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s) {
   if (a.st_part) {
     SAD_REQUIRE(!a.res && !a.relu && a.st_rows, "fused BN statistics: raw conv (no residual / ReLU), st_rows set");
