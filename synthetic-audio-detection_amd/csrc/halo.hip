@@ -726,8 +726,13 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       // next tile's patch: one piece per tap over taps 0..QP-1; this tile's
       // residual: fragment j at tap j
-      if constexpr (k < QP)
-        if (has_next) patch_piece(k, pb ^ 1);
+      // the next tile's patch, all pieces at tap 0: the stamps showed the
+      // early waves waiting ~1.1k cycles for pieces issued at taps 0..5
+      if constexpr (k == 0)
+        if (has_next) {
+#pragma unroll
+          for (int kk = 0; kk < QP; ++kk) patch_piece(kk, pb ^ 1);
+        }
       if constexpr (k < TP) load_res(t, k);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (k < 8) {
