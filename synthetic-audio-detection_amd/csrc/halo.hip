@@ -997,8 +997,13 @@ __global__ __launch_bounds__(512, 1) void halo_rw_x3_kernel(BlockConvArgs a) {
     static_for<9>([&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (k < QP)
-        if (issue) patch_piece(po, k, ich);
+      // the other chunk's pieces all at tap 0 (as variant 25: a piece issued at
+      // tap 5 had too little of the chunk left to land)
+      if constexpr (k == 0)
+        if (issue) {
+#pragma unroll
+          for (int kk = 0; kk < QP; ++kk) patch_piece(po, kk, ich);
+        }
       if constexpr (RES && k >= QP && k < QP + TP)
         if (res_t >= 0) load_res(res_t, k - QP);
       __builtin_amdgcn_sched_barrier(0);
