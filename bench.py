@@ -50,7 +50,7 @@ F32_PEAK_TFLOPS = 157.3        # f32 MFMA = f32 vector peak (MI355X_MICROARCH.md
 DOMINANT_VARIANT = 13
 DOMINANT_KERNEL = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1, false, false, false>|131072'
 DOMINANT_KERNEL_OLD = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1, false>|131072'
-TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r02s3_pmc_traffic_final.json', 'r02s3_pmc_traffic_boxC.json', 'r02_pmc_traffic.json', 'r01_pmc_traffic.json')
+TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r02s3_pmc_traffic_final.json', 'r02_pmc_traffic.json', 'r01_pmc_traffic.json')
                      if os.path.exists(os.path.join(ROOT, 'profiles', f))), '')
 FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats
 FE_BYTES = 256000 + 128512     # int16 PCM read + fp32 [128, 251] map written
