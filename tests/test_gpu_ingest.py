@@ -253,3 +253,17 @@ def test_main_empty_resampled_file(tmp_path):
     out = tmp_path / 'o.json'
     js = ir.main(['--merged-model', str(mp), '--audio', str(p), '--output-json', str(out)])
     assert js == {'filename': str(p), 'segments': [], 'percentages': {}}
+
+
+def test_select_windows_edges():
+    """slice_waveform's edge behaviour on the device path: overlap 1.0 gives a
+    zero hop (range() refuses it, so ValueError), a waveform shorter than one
+    window gives no windows, exactly one window gives one."""
+    from sad import ingest
+    x = torch.full((128000,), 0.5, device=DEV)
+    with pytest.raises(ValueError):
+        ingest.select_windows(x, 32000, 4.0, 1.0, 1e-3)
+    assert ingest.select_windows(x[:127999].contiguous(), 32000, 4.0, 0.0, 1e-3) == ([], [])
+    assert ingest.select_windows(x, 32000, 4.0, 0.85, 1e-3) == ([0], [0.0])
+    with pytest.raises(ValueError):
+        ingest.Windows(x, [1], 128000)  # past the end
