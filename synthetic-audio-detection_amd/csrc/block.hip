@@ -27,7 +27,9 @@
 //    (64 bf16 / 32 f32), 8 x 16-B chunks per pixel row, XOR-swizzled through
 //    the DMA source address (LDS-DMA writes lane-linearly).
 #include <stdio.h>
+#include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 #include <vector>
 
@@ -113,6 +115,7 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wave / WP, wp = wave % WP;
+  SAD_CLOCK_STAMP(0);
   const int n_tc = a.Cout / BC;
   const int w = xcd_remap(blockIdx.x, gridDim.x);
   // channel tile tc = w % n_tc: both channel tiles share an XCD's pixel tiles.
@@ -595,6 +598,7 @@ if constexpr (X3) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  SAD_CLOCK_STAMP(1);
   if constexpr (ST) {  // fold the WP pixel waves of each channel
     __syncthreads();
     stat_rows_write(s_stat, WP, BC, a.st_part, wi, a.Cout, c0, tid, 64 * NW);
@@ -797,10 +801,50 @@ static bool variant_fits(int v, int cout) {
 #if SAD_STAMPS
 // diagnostic build: stamp the launch, synchronise, print the per-step phase
 // averages (cycles) of wave 0 and wave NW/2 of workgroup 0 to stderr
+constexpr size_t kStampWords = SAD_CLOCK_BASE + 4 * SAD_CLOCK_WGS;
+// SAD_STAMP_EVERY=n: stamp only every n-th launch of a stamped variant (the
+// others run unstamped and unsynchronised, so a loop keeps the chip loaded)
+static bool stamp_this_launch(int which) {  // counted per stamped variant
+  static const int every = [] {
+    const char* e = getenv("SAD_STAMP_EVERY");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
+  static long count[2] = {0, 0};
+  return count[which]++ % every == every - 1;
+}
 static int stamp_report(const BlockConvArgs& a, hipStream_t s) {
-  std::vector<uint64_t> h(2 * 4096);
+  std::vector<uint64_t> h(kStampWords);
   SAD_CHECK_HIP(hipStreamSynchronize(s));
   SAD_CHECK_HIP(hipMemcpy(h.data(), a.stamps, h.size() * 8, hipMemcpyDeviceToHost));
+  {  // in-kernel clock over workgroups; ramp and tail from the 100 MHz clock
+    std::vector<double> clk, dur, xcd[8];
+    uint64_t r0 = ~0ull, r0max = 0, r1min = ~0ull, r1 = 0;
+    for (int g = 0; g < SAD_CLOCK_WGS; ++g) {
+      const uint64_t* c = &h[SAD_CLOCK_BASE + 4 * g];
+      if (!c[0] || !c[2] || c[3] <= c[1]) continue;
+      clk.push_back((double)(c[2] - c[0]) / (double)(c[3] - c[1]) * 100.0);  // MHz
+      xcd[g % 8].push_back(clk.back());  // workgroups go round-robin over the 8 XCDs
+      dur.push_back((double)(c[3] - c[1]) / 100.0);                          // us
+      r0 = std::min(r0, c[1]); r0max = std::max(r0max, c[1]);
+      r1min = std::min(r1min, c[3]); r1 = std::max(r1, c[3]);
+    }
+    if (!clk.empty()) {
+      std::sort(clk.begin(), clk.end());
+      std::sort(dur.begin(), dur.end());
+      fprintf(stderr, "clock M=%lld Cout=%d: %zu workgroups, in-kernel clock median %.0f MHz (min %.0f, max %.0f); "
+              "span %.1f us, workgroup time median %.1f us (min %.1f, max %.1f), starts spread %.1f us, "
+              "ends spread %.1f us\n", (long long)a.M, a.Cout, clk.size(), clk[clk.size() / 2], clk.front(),
+              clk.back(), (r1 - r0) / 100.0, dur[dur.size() / 2], dur.front(), dur.back(), (r0max - r0) / 100.0,
+              (r1 - r1min) / 100.0);
+      fprintf(stderr, "clock per XCD (median MHz):");
+      for (auto& x : xcd) {
+        if (x.empty()) continue;
+        std::sort(x.begin(), x.end());
+        fprintf(stderr, " %.0f", x[x.size() / 2]);
+      }
+      fprintf(stderr, "\n");
+    }
+  }
   for (int w = 0; w < 2; ++w) {
     double ph[4] = {0, 0, 0, 0};
     int n = 0;
@@ -896,8 +940,9 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
     SAD_REQUIRE(halo_ok(a, dtype), "halo conv (variant 25): bf16, 3x3/s1/p1, no GEMM shortcut, H, W % 16");
 #if SAD_STAMPS
     static uint64_t* stamp_buf25 = nullptr;
-    if (!stamp_buf25) SAD_CHECK_HIP(hipMalloc(&stamp_buf25, 2 * 4096 * 8));
-    SAD_CHECK_HIP(hipMemsetAsync(stamp_buf25, 0, 2 * 4096 * 8, s));
+    if (!stamp_this_launch(0)) return launch_halo_rw(a, s);
+    if (!stamp_buf25) SAD_CHECK_HIP(hipMalloc(&stamp_buf25, kStampWords * 8));
+    SAD_CHECK_HIP(hipMemsetAsync(stamp_buf25, 0, kStampWords * 8, s));
     a.stamps = stamp_buf25;
     const int rc25 = launch_halo_rw(a, s);
     return rc25 == SAD_OK ? stamp_report(a, s) : rc25;
@@ -912,9 +957,11 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   SAD_REQUIRE(!a.res || a.res_pstride % 4 == 0, "residual pixel stride must keep 4-channel alignment");
 #if SAD_STAMPS
   static uint64_t* stamp_buf = nullptr;
-  if (!stamp_buf) SAD_CHECK_HIP(hipMalloc(&stamp_buf, 2 * 4096 * 8));
-  SAD_CHECK_HIP(hipMemsetAsync(stamp_buf, 0, 2 * 4096 * 8, s));
-  a.stamps = stamp_buf;
+  if (v == 13 && stamp_this_launch(1)) {
+    if (!stamp_buf) SAD_CHECK_HIP(hipMalloc(&stamp_buf, kStampWords * 8));
+    SAD_CHECK_HIP(hipMemsetAsync(stamp_buf, 0, kStampWords * 8, s));
+    a.stamps = stamp_buf;
+  }
 #endif
   int rc;
   if (dtype == SAD_BF16X3) {
@@ -924,7 +971,7 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
     rc = dtype == SAD_BF16 ? launch_block_v<u16>(a, v, s) : launch_block_v<float>(a, v, s);
   }
 #if SAD_STAMPS
-  if (rc == SAD_OK && v == 13) rc = stamp_report(a, s);
+  if (rc == SAD_OK && a.stamps) rc = stamp_report(a, s);
 #endif
   return rc;
 }

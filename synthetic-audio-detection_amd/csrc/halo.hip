@@ -542,6 +542,7 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool early = wave < 4;  // epilogue before the tile barrier
   const int wp = wave;          // tile rows 2wp, 2wp+1; all 64 channels
+  SAD_CLOCK_STAMP(0);
   const int w = xcd_remap(blockIdx.x, gridDim.x);
   const int tiles_x = a.W / TW, tiles_img = tiles_x * (a.H / TH);
   const int tiles_p = a.N * tiles_img;
@@ -767,6 +768,7 @@ __global__ __launch_bounds__(512, 1) void halo_rw_kernel(BlockConvArgs a) {
     pb ^= 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  SAD_CLOCK_STAMP(1);
   if constexpr (ST) {  // the resident weights are done: fold the 8 pixel waves
     __syncthreads();
     float* s_red = (float*)smem;

@@ -6,6 +6,26 @@
 
 namespace sad {
 
+// Diagnostic builds (-DSAD_STAMPS=1): wave 0 of every workgroup records
+// (s_memtime, s_memrealtime) at kernel entry (slot 0) and exit (slot 1) in
+// a.stamps[SAD_CLOCK_BASE + 4 * blockIdx.x + 2 * slot ..]: the in-kernel clock
+// (MI355X_MICROARCH.md 'DVFS give-back' item 6) and the launch's ramp and tail.
+#define SAD_CLOCK_BASE 8192
+#define SAD_CLOCK_WGS 4096
+#define SAD_CLOCK_STAMP(slot)                                                                      \
+  do {                                                                                             \
+    if constexpr (SAD_STAMPS) {                                                                    \
+      if (a.stamps && wave == 0 && blockIdx.x < SAD_CLOCK_WGS) {                                   \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                          \
+        const uint64_t r_ = __builtin_amdgcn_s_memrealtime();                                      \
+        if (lane == 0) {                                                                           \
+          a.stamps[SAD_CLOCK_BASE + 4 * blockIdx.x + 2 * (slot)] = t_;                             \
+          a.stamps[SAD_CLOCK_BASE + 4 * blockIdx.x + 2 * (slot) + 1] = r_;                         \
+        }                                                                                          \
+      }                                                                                            \
+    }                                                                                              \
+  } while (0)
+
 struct ConvArgs {
   const void* in;        // NHWC [N, H, W, *] with pixel stride in_pstride (elements)
   int64_t in_pstride;

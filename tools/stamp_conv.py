@@ -10,7 +10,14 @@ a -DSAD_STAMPS=1 build of libsad (SAD_LIB=abl/libsad_stamps.so):
 The library prints one line per launch and wave to stderr.  Variant 25 phases
 per tile: 0-1 taps issued, 1-2 epilogue (early waves) / wait, 2-3 tile barrier,
 3-next late epilogue.  Variant 13 per K-step: wait+barrier, reads+DMA, MFMA
-issue, tail.  Stamping costs about 11 % of wave cycles."""
+issue, tail.  Stamping costs about 11 % of wave cycles.
+
+The same build also stamps (s_memtime, s_memrealtime) at entry and exit of
+wave 0 of every workgroup and prints the in-kernel clock (median and per XCD),
+the launch span and the spread of workgroup end times.  For the clock under
+load, stamp every n-th launch inside the bench loop instead:
+
+    SAD_LIB=abl/libsad_stamps.so SAD_STAMP_EVERY=1000 python bench.py --kernels-only --steps 300"""
 import os
 import sys
 
