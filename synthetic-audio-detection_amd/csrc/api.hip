@@ -445,6 +445,8 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
 // ramp and tail).  Same-box sweeps (tools/frontmb_ab.sh, "front:micro-batch"):
 // 32:512 46.9k seg/s vs 0:128 45.9k, 0:512 44.4-46.4k, 64:512 45.4k; 16 is 7%
 // slower (layer2's grids underfill).  At 32:128 one box measured -1.1%.
+// Round 2 at micro-batch 1024: 40 is 0.9 % and 48 1.4 % slower than 32 (same
+// box, 3 rounds; profiles/r02s3_frontmb_ab.log).
 static int front_sub_batch() {
   static int v = [] {
     const char* e = getenv("SAD_FRONT_MB");
