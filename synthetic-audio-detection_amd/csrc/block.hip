@@ -695,6 +695,8 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
 }
 
 int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s, bool x3 = false);
+int launch_halo256(const BlockConvArgs& a, hipStream_t s, bool x3);
+bool halo256_ok(const BlockConvArgs& a);
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s);
 int launch_halo_rw_x3(const BlockConvArgs& a, hipStream_t s);
 
@@ -747,6 +749,16 @@ static bool x3_rw() {
   }();
   return v;
 }
+// SAD_HALO256=1 runs layer3/4's stride-1 convs on the patch-resident variant
+// 30 instead of the implicit GEMM (variant 13) (A/B switch; off by default
+// until it measures faster)
+static bool halo256_on() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_HALO256");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return v;
+}
 static int block_device_cus() {
   static int cus[64] = {};
   int dev = 0;
@@ -764,6 +776,7 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   if (dtype == SAD_BF16X3) {
     // layer1 (64 -> 64): the resident-weight split-bf16 kernel (half the channels per workgroup)
     if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64 && x3_rw()) return 26;
+    if (halo256_on() && halo256_ok(a)) return 30;
     return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   }
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
@@ -773,6 +786,7 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   // leave CUs idle (one workgroup per CU), so split the channel tile (variant
   // 15, 128x256).  Both keep the 256-pixel tile and the same K order, so the
   // results (incl. the fused average pool) do not depend on the choice.
+  if (halo256_on() && halo256_ok(a)) return 30;  // layer3/4 stride-1 convs: patch-resident 256 x 256
   if (a.Cout % 256 == 0)
     return a.res || (a.M + 255) / 256 * (a.Cout / 256) >= block_device_cus() ? 13 : 15;  // 13: residual epilogue
   return a.Cout % 128 == 0 ? c128_variant() : 9;
@@ -780,7 +794,7 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
 // pixel tile of the variants that can fuse the average pool (0: cannot)
 static int pool_tile(int v) {
   switch (v) {
-    case 13: case 14: case 15: return 256;
+    case 13: case 14: case 15: case 30: return 256;
     case 16: return 512;
   }
   return 0;
@@ -791,6 +805,7 @@ bool block_conv_can_pool(const BlockConvArgs& a, int dtype) {
 }
 static bool variant_fits(int v, int cout) {
   if (v == 26) return cout == 64;
+  if (v == 30) return cout % 256 == 0;
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128, 128};
   if (v == 20 || v == 21) return cout % 64 == 0;
   if (v == 22) return cout % 128 == 0;
@@ -928,6 +943,20 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   if (a.M == 0) return SAD_OK;
   const int v = variant > 0 ? variant : default_block_variant(a_in, dtype);
   SAD_REQUIRE(variant_fits(v, a.Cout), "variant's channel tile does not divide Cout");
+  if (v == 30) {
+    SAD_REQUIRE(dtype != SAD_F32 && halo256_ok(a_in), "variant 30: bf16 / split-bf16 3x3/s1/p1, Cout % 256, 16 x 16 tiles");
+#if SAD_STAMPS
+    static uint64_t* stamp_buf30 = nullptr;
+    if (!stamp_this_launch(1)) return launch_halo256(a, s, dtype == SAD_BF16X3);
+    if (!stamp_buf30) SAD_CHECK_HIP(hipMalloc(&stamp_buf30, kStampWords * 8));
+    SAD_CHECK_HIP(hipMemsetAsync(stamp_buf30, 0, kStampWords * 8, s));
+    a.stamps = stamp_buf30;
+    const int rc30 = launch_halo256(a, s, dtype == SAD_BF16X3);
+    return rc30 == SAD_OK ? stamp_report(a, s) : rc30;
+#else
+    return launch_halo256(a, s, dtype == SAD_BF16X3);
+#endif
+  }
   if (dtype == SAD_BF16X3 && v == 26) {
     SAD_REQUIRE(halo_ok(a_in, dtype), "split-bf16 halo conv: 3x3/s1/p1, H, W % 16");
     return launch_halo_rw_x3(a, s);

@@ -42,6 +42,9 @@ def _conv_ref(x, w, stride, pad, sc=None, wsc=None, sc_stride=1, bias=None, relu
     (64, 128, 32, 2, 'downsample', 0),  # layer2.0 conv2 + downsample: variant 15
     (128, 256, 16, 1, None, 0),         # variant 13 (256x256 rolling prefetch)
     (256, 256, 16, 1, 'identity', 13),
+    (256, 256, 16, 1, 'identity', 30),  # patch-resident 256 x 256 (halo256.hip)
+    (128, 256, 32, 2, 'downsample', 30),
+    (256, 512, 32, 1, None, 30),
     (128, 128, 16, 1, None, 10),
 ])
 def test_block_conv_x3_vs_float64(cin, cout, H, stride, shortcut, variant):
