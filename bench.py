@@ -116,7 +116,11 @@ def cpu_baseline(n_clips: int = 64, passes: int = 2):
     return {'value': round(n / t_mem, 2), 'unit': 'segments/s', 'cores': torch.get_num_threads(), 'kind': 'port',
             'value_incl_wav_decode': round(n / t_wav, 2),
             'host': {'os_cpu_count': os.cpu_count(), 'torch_threads': torch.get_num_threads(),
-                     'cpu_model': cpu_model()},
+                     'cpu_model': cpu_model(),
+                     'threads_note': 'torch_threads = the CPU share one GPU gets on this box (the pool sets '
+                                     'OMP_NUM_THREADS to 16 per GPU; os.cpu_count() counts the whole host, '
+                                     'whose other cores belong to the other 7 GPUs); the reference runs '
+                                     'inference single-process on the same share'},
             'sample': f'configs[0]: {n_clips} synthetic 4 s / 32 kHz clips x {passes} passes through the CPU '
                       f'oracle (per-window mel/dB/std/resize/repeat(3), windows batched by 128, 1 sub-model '
                       f'ResNet-18 + head, fp32): {t_mem:.1f} s from decoded waveforms; {t_wav:.1f} s from the WAV '
@@ -371,7 +375,8 @@ def main():
                          'kernel': 'sad::block_conv_kernel 256x256 tile (variant 13): the layer3 + layer4 convs, '
                                    '8 launches per micro-batch, about 35% of the bf16 step',
                          'achieved': round(exe, 1), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(exe / peak, 4),
-                         'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, '
+                         'traffic': traffic, 'traffic_unit': 'memory-side bytes per launch = L2-miss traffic, Infinity-Cache hits '
+                                                             'included (FETCH_SIZE x2 + WRITE_SIZE, '
                                                              + os.path.relpath(TRAFFIC_JSON, ROOT) + ')',
                          **kinfo,
                          'backbone': {'achieved': round(bb_alg * fac, 1), 'frac': round(bb_alg * fac / peak, 4),

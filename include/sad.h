@@ -52,6 +52,10 @@ enum sad_dtype {
 /* ---------------------------------------------------------------- runtime */
 /* Select the device for this thread's subsequent plan creation. */
 int sad_init(int device);
+/* Wait for the device, then release what the library itself holds (the
+ * launch-timing events of an unfinished sad_profile_begin).  Plans are
+ * caller-owned: destroy them first.  sad_init may be called again after it. */
+int sad_shutdown(void);
 const char* sad_last_error(void);
 /* Library / kernel build identification (for provenance in bench output). */
 const char* sad_version(void);
@@ -80,7 +84,10 @@ int sad_frontend_plan_destroy(sad_frontend_plan* plan);
 int sad_frontend_frames(const sad_frontend_plan* plan, int32_t* n_frames);
 
 /* pcm: int16 mono segments, segment i at pcm + i*seg_stride (elements),
- *      n_samples each (stereo callers average on the host first);
+ *      n_samples each.  There is no n_ch argument: multi-channel audio goes
+ *      through sad_pcm_mono_run first, once per file, as the reference
+ *      averages the whole waveform before slicing it (inference_runner.py:145-146);
+ *      averaging per segment would redo it for every overlapping window;
  * out_db:  optional [n_seg, n_mels, n_frames] fp32 dB map after the top-db
  *          clamp (NULL to skip);
  * out_map: [n_seg, n_mels, n_frames] fp32 standardised map
@@ -108,7 +115,7 @@ enum sad_pcm_format {
   SAD_PCM_I16 = 0, /* int16, scaled by 1/32768 (torchaudio.load normalize=True) */
   SAD_PCM_F32 = 1  /* fp32 (other WAV encodings, decoded on the host) */
 };
-/* out[i] = mean_c pcm[i][c] (waveform.mean(dim=0): fp32 sum x 1/C) for
+/* out[i] = mean_c pcm[i][c] (waveform.mean(dim=0): channels summed in order, / C) for
  * i < frames, 0 for frames <= i < out_len (the zero pad to one window, :151-154). */
 int sad_pcm_mono_run(const void* pcm, int32_t format, int64_t frames, int32_t channels, float* out,
                      int64_t out_len, void* stream);

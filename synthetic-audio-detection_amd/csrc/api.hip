@@ -339,6 +339,21 @@ extern "C" int sad_profile_begin(void) {
   return SAD_OK;
 }
 
+// sad_shutdown: release what the library itself holds (the launch-timing
+// events of an unfinished sad_profile_begin) after the device has drained.
+// Plans are caller-owned and destroyed by their *_destroy calls.
+extern "C" int sad_shutdown(void) {
+  SAD_CHECK_HIP(hipDeviceSynchronize());
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto& r : g_prof) {
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+  }
+  g_prof.clear();
+  g_prof_on = false;
+  return SAD_OK;
+}
+
 extern "C" int sad_profile_end(int32_t variant, double* total_ms, int64_t* launches, double* flops) {
   SAD_REQUIRE(total_ms && launches && flops, "null outputs");
   std::lock_guard<std::mutex> lk(g_prof_mu);

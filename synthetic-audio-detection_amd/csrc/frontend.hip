@@ -160,8 +160,12 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
   float2* buf = s_buf[wave];
   float* pw = s_pow[wave];
   const int pad = FE_NFFT / 2;
-  // aligned pair loads need an even sample offset for every frame and pair
-  const bool pairs = ((hop & 1) == 0) && ((seg_stride & 1) == 0) && ((((uintptr_t)pcm) & (2 * sizeof(IT) - 1)) == 0);
+  // aligned pair loads need an even sample offset for every frame and pair:
+  // even hop, and an even segment start (seg_stride in strided mode; this
+  // segment's own offset in windows mode, where seg_stride is 0 and an odd
+  // window hop gives odd starts) -- else the scalar path
+  const bool pairs = ((hop & 1) == 0) && ((seg_stride & 1) == 0) && ((x0 & 1) == 0) &&
+                     ((((uintptr_t)pcm) & (2 * sizeof(IT) - 1)) == 0);
 
   // int16 path: the next frame's PCM pairs are loaded while this frame is
   // transformed (software pipeline: a frame's HBM latency no longer stalls its

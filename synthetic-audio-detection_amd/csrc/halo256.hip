@@ -127,8 +127,7 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
     }
     return 9 * cinb + (s - 9 * nc0) * 128;
   };
-  auto issue_weights = [&](int step_in_tile, int stage) __attribute__((always_inline)) {
-    const int kb = step_kb(step_in_tile);
+  auto issue_weights = [&](int kb, int stage) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < QW; ++i) {
       const int q = lw + 4 * i;
@@ -143,27 +142,26 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
     oy0 = (rem / tiles_x) * TH;
     ox0 = (rem - (rem / tiles_x) * tiles_x) * TW;
   };
-  auto patch_piece = [&](int t, int c, int k, int buf) __attribute__((always_inline)) {
+  // The tile origin is wave-uniform and computed once per chunk issue (scalar
+  // divisions); a piece then costs ~10 VALU.  (Recomputing the origin per piece
+  // made the patch waves' issue VALU-bound: l4.c2 1105 -> 932 us with the patch
+  // DMA ablated.)
+  auto patch_piece = [&](int yb, int xb, int base, int lr, int k, int buf) __attribute__((always_inline)) {
     const int q = lw + 4 * k;
     if (NDP % 4 == 0 || q < NDP) {
-      int b, oy0, ox0;
-      tile_origin(t, b, oy0, ox0);
-      const int pr = 8 * q + lrow;
+      const int pr = 8 * q + lr;
       const int py = pr / PW, px = pr - py * PW;
-      const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+      const int iy = yb + py, ix = xb + px;
       const int off = (pr < PR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
-                          ? ((b * a.H + iy) * a.W + ix) * ps0 + c * 128 + sw16
+                          ? base + (py * a.W + px) * ps0
                           : BAD;
       dma16_m0(r0, off, lds0 + OFF_P + buf * PATCH + q * 1024);
     }
   };
-  auto sc_piece = [&](int t, int s, int k, int buf) __attribute__((always_inline)) {
+  auto sc_piece = [&](int base, int k, int buf) __attribute__((always_inline)) {
     const int q = lw + 4 * k;
-    int b, oy0, ox0;
-    tile_origin(t, b, oy0, ox0);
     const int r = 8 * q + lrow, ty = r >> 4, tx = r & 15;
-    const int iy = (oy0 + ty) * a.ss1, ix = (ox0 + tx) * a.ss1;
-    dma16_m0(r1, ((b * a.H1 + iy) * a.W1 + ix) * ps1 + s * 128 + sw16, lds0 + OFF_P + buf * PATCH + q * 1024);
+    dma16_m0(r1, base + (ty * a.W1 + tx) * (a.ss1 * ps1), lds0 + OFF_P + buf * PATCH + q * 1024);
   };
   // chunk u of the workgroup's sequence (per tile: nc0 patch chunks, then nk1 shortcut chunks)
   struct Chunk {
@@ -179,14 +177,26 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   // pieces k = tap, tap + 4, ... of chunk x (all of them when tap < 0) into buffer buf
   auto issue_chunk = [&](Chunk x, int buf, int tap) __attribute__((always_inline)) {
     if (x.t >= tp_end) return;
+    int b, oy0, ox0;
+    tile_origin(__builtin_amdgcn_readfirstlane(x.t), b, oy0, ox0);
+    b = __builtin_amdgcn_readfirstlane(b);
+    oy0 = __builtin_amdgcn_readfirstlane(oy0);
+    ox0 = __builtin_amdgcn_readfirstlane(ox0);
+    // lane row through an opaque move: the compiler would otherwise hoist every
+    // piece's (py, px) out of the K loop into registers and spill
+    int lr;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lr) : "v"(lrow));
     if (x.c < nc0) {
+      // patch row py, column px at input (oy0 - 1 + py, ox0 - 1 + px)
+      const int base = ((b * a.H + oy0 - 1) * a.W + ox0 - 1) * ps0 + x.c * 128 + sw16;
 #pragma unroll
       for (int k = 0; k < QP; ++k)
-        if (tap < 0 || k % 4 == tap) patch_piece(x.t, x.c, k, buf);
+        if (tap < 0 || k % 4 == tap) patch_piece(oy0 - 1, ox0 - 1, base, lr, k, buf);
     } else {
+      const int base = ((b * a.H1 + oy0 * a.ss1) * a.W1 + ox0 * a.ss1) * ps1 + (x.c - nc0) * 128 + sw16;
 #pragma unroll
       for (int k = 0; k < QS; ++k)
-        if (tap < 0 || k % 4 == tap) sc_piece(x.t, x.c - nc0, k, buf);
+        if (tap < 0 || k % 4 == tap) sc_piece(base, k, buf);
     }
   };
 
@@ -197,7 +207,7 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   // ---- prologue: weights of step 0, patch of the first chunk
   Chunk cur{tp_begin, 0};
   if (wloader)
-    issue_weights(0, 0);
+    issue_weights(step_kb(0), 0);
   else
     issue_chunk(cur, 0, -1);
 
@@ -224,11 +234,13 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
     }
   };
   const int ab = a.ablate;  // timing ablations (wrong results): 1 no DMA in the loop, 2 no waits,
-                            // 4 no barrier, 8 no epilogue, 16 no weight DMA, 32 no patch DMA
+                            // 4 no barrier, 8 no epilogue, 16 no weight DMA, 32 no patch DMA;
+                            // 64: patch pieces at the step's top (same results)
   // weight fragment rows wc*128 + i*16 + fr: slot = chunk ^ (fr & 6)
   const int wsl0 = (fg ^ (fr & 6)) << 4, wsl1 = ((fg + 4) ^ (fr & 6)) << 4;
   const int wrow0 = (wc * 16 * TC + fr) * 128;
 
+  int kb_next = 0;  // K byte offset of the next step's weights (set by the loop)
   // ---- one K-step: fragments from weight stage `ws` and pixel rows prow(j)
   // of patch buffer `pb`; the weight waves issue the next step's weights after
   // their half-0 fragment reads (overlapping their latency), the patch waves
@@ -236,6 +248,10 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   auto compute = [&](int ws, int pbuf, auto prow, auto late) __attribute__((always_inline)) {
     const char* wb = smem + ws * WST + wrow0;
     const char* pb = smem + OFF_P + pbuf * PATCH;
+    // ablate bit 64 (A/B): the patch waves issue their pieces at the top of
+    // the step, ahead of the weight waves' burst in the CU's DMA queue
+    if (!wloader && (ab & 64) && !(ab & 33)) late();
+    __builtin_amdgcn_sched_barrier(0);
     uint4 wf[TC], pf[TP], pg[TP];
 #pragma unroll
     for (int i = 0; i < TC; ++i) wf[i] = *(const uint4*)(wb + i * 16 * 128 + wsl0);
@@ -244,7 +260,7 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
       const int r = prow(j);
       pf[j] = *(const uint4*)(pb + r * 128 + ((fg ^ (r & 6)) << 4));
     }
-    if (wloader && g + 1 < total && !(ab & 17)) issue_weights(g + 1 - (g + 1) / nk * nk, (g + 1) & 1);
+    if (wloader && g + 1 < total && !(ab & 17)) issue_weights(kb_next, (g + 1) & 1);
     __builtin_amdgcn_sched_barrier(0);
     stamp(2);
 #pragma unroll
@@ -271,7 +287,7 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!wloader && !(ab & 33)) late();
+    if (!wloader && !(ab & 97)) late();
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (SR < TC) {
 #pragma unroll
@@ -388,6 +404,15 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   Chunk nx = next_chunk(cur);
   for (; g < total;) {
     const bool sc = c >= nc0;  // shortcut chunk (1 step)
+    // K byte offset of the next step's weights (scalar, no division per step)
+    if (!sc && tap < 8)
+      kb_next = (tap + 1) * cinb + c * 128;
+    else if (c + 1 < nc0)
+      kb_next = (c + 1) * 128;
+    else if (c + 1 < nc0 + nk1)
+      kb_next = 9 * cinb + (c + 1 - nc0) * 128;
+    else
+      kb_next = 0;
     top(tap == 0);
     const int ky = tap / 3, kx = tap - 3 * (tap / 3);
     const int rb = sc ? wp * TP * 16 + fr : (wp * TP + ky) * PW + kx + fr;  // fragment 0's pixel row

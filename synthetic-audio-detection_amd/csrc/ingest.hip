@@ -28,12 +28,15 @@
 namespace sad {
 
 // ---- interleaved PCM [frames][channels] -> mono fp32 [out_len] -------------
-// out[i] = (sum_c x[i][c]) * (1/C) for i < frames, 0 for frames <= i < out_len.
-// ATen's mean multiplies the fp32 sum by 1/C; int16 is scaled by 1/32768 first
-// (torchaudio.load normalize=True), so C = 1, 2, 4 are bit-exact with the host.
+// out[i] = (sum_c x[i][c]) / C for i < frames, 0 for frames <= i < out_len.
+// The reference's waveform.mean(dim=0) runs on the CPU, where ATen's mean is
+// sum(dim).div_(C): channels summed in order, then a true fp32 division (not a
+// multiply by 1/C, which differs by an ulp for C = 3, 5, 6, ...); int16 is
+// scaled by 1/32768 first (torchaudio.load normalize=True).  Bit-exact with
+// the host for every channel count.
 template <typename IT>
 __global__ __launch_bounds__(256) void pcm_mono_kernel(const IT* __restrict__ x, int64_t frames, int channels,
-                                                       float inv_c, float* __restrict__ out, int64_t out_len) {
+                                                       float fc, float* __restrict__ out, int64_t out_len) {
   const float scale = sizeof(IT) == 2 ? (1.0f / 32768.0f) : 1.0f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < out_len;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -42,7 +45,7 @@ __global__ __launch_bounds__(256) void pcm_mono_kernel(const IT* __restrict__ x,
       const IT* p = x + i * channels;
       float s = (float)p[0] * scale;
       for (int c = 1; c < channels; ++c) s += (float)p[c] * scale;
-      v = channels == 1 ? s : s * inv_c;
+      v = channels == 1 ? s : s / fc;
     }
     out[i] = v;
   }
@@ -182,13 +185,13 @@ extern "C" int sad_pcm_mono_run(const void* pcm, int32_t format, int64_t frames,
   if (out_len == 0) return SAD_OK;
   SAD_REQUIRE(out && (pcm || frames == 0), "null pointer");
   hipStream_t s = (hipStream_t)stream;
-  const float inv_c = 1.0f / (float)channels;
+  const float fc = (float)channels;
   if (format == SAD_PCM_I16)
     hipLaunchKernelGGL(pcm_mono_kernel<int16_t>, dim3(grid_for(out_len)), dim3(256), 0, s, (const int16_t*)pcm,
-                       frames, channels, inv_c, out, out_len);
+                       frames, channels, fc, out, out_len);
   else
     hipLaunchKernelGGL(pcm_mono_kernel<float>, dim3(grid_for(out_len)), dim3(256), 0, s, (const float*)pcm, frames,
-                       channels, inv_c, out, out_len);
+                       channels, fc, out, out_len);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }

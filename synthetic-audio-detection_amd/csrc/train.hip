@@ -9,13 +9,15 @@
 // folds BN into the convs; training cannot, so a train-mode conv is
 //   raw conv (conv_igemm_kernel, bias 0)  ->  bn_stats  ->  bn_apply(+res, ReLU)
 // and the backward pass is
-//   bn_backward (reduce + finalize + apply)  ->  dgrad (conv_igemm_kernel on
-//   flipped weights, or GEMM + col2im for stride 2)  ->  wgrad (im2col + GEMM).
+//   bn_backward (reduce + finalize + apply)  ->  dgrad (the forward conv kernels
+//   on flipped, transposed weights; stride 2: a pixel-axis GEMM + col2im)  ->
+//   wgrad (the pixel-axis GEMM, wgrad.hip).
 //
 // Kernels here are HBM-bound elementwise / reduction passes over NHWC
 // activations (8 channels = 16 B (bf16) per thread, coalesced); the dense
-// contractions are the MFMA conv kernel (conv.hip) and, for the two GEMMs that
-// are plain library GEMMs after im2col (wgrad, strided dgrad), rocBLAS.
+// contractions are hand-written MFMA kernels: the conv kernels (conv.hip,
+// block.hip, halo.hip) and kouter_bf16_kernel (wgrad.hip) for the weight
+// gradient and the stride-2 input gradient.  No BLAS library is linked.
 #include <math.h>
 
 #include <vector>
@@ -890,7 +892,14 @@ extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_
   a.M = N * a.Ho * a.Wo;
   const int64_t P = a.M;
   const int v = default_block_variant(a, dtype);
-  const bool fused = dtype == SAD_BF16 && (v == 13 || v == 15 || v == 20 || v == 25);
+  // The fused statistics need ONE launch (one partial row per workgroup).  A
+  // batch whose operands pass the kernels' 32-bit buffer range (e.g. a
+  // Bottleneck's 256-channel 128^2 layer1 maps at ~256 images) is split by
+  // launch_block_conv into image-range launches, so it takes the unfused path:
+  // plain conv launches, then bn_reduce over the stored output.
+  const int64_t es = dtype == SAD_F32 ? 4 : 2, lim = (1ll << 31) - 65536;
+  const bool one_launch = N * H * W * Cin * es < lim && a.M * Cout * es < lim;
+  const bool fused = dtype == SAD_BF16 && one_launch && (v == 13 || v == 15 || v == 20 || v == 25);
   int rows = 0;
   if (fused) {
     a.st_part = ws;

@@ -47,6 +47,7 @@ class PackSeg(ctypes.Structure):
 
 SIGNATURES = {
     'sad_init': (ctypes.c_int, [ctypes.c_int]),
+    'sad_shutdown': (ctypes.c_int, []),
     'sad_last_error': (ctypes.c_char_p, []),
     'sad_version': (ctypes.c_char_p, []),
     'sad_frontend_plan_create': (ctypes.c_int, [ctypes.POINTER(FrontendCfg), ctypes.POINTER(P)]),

@@ -28,6 +28,10 @@ DEV = 'cuda:0'
     ('bf16', 4, 16, 256, 256, 3, 1, 1, 1),     # tiny map: variant 15
     ('bf16', 4, 32, 64, 64, 3, 2, 1, 0),       # Cout 64, stride 2: variant 9, conv + bn_reduce
     ('fp32', 2, 16, 256, 256, 3, 1, 1, 0),     # fp32: conv + bn_reduce
+    # a Bottleneck layer1 conv3 (1x1, 64 -> 256 at 128^2) at 260 images: the
+    # 2.18 GB output passes the 32-bit buffer range, so the conv runs as
+    # image-range launches and the statistics take the unfused bn_reduce path
+    ('bf16', 260, 128, 64, 256, 1, 1, 0, 0),
 ])
 def test_conv_bn_train_vs_float64(dtype, N, H, cin, cout, k, stride, pad, fused):
     from sad import _lib

@@ -1,0 +1,7 @@
+set -o pipefail
+cd /root/repo; mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_blockconv.py tests/test_gpu_x3.py tests/test_gpu_ingest.py -k "30 or mono or windows" > gpurun_out/r03_m2_tests.log 2>&1 || { tail -30 gpurun_out/r03_m2_tests.log; exit 1; }
+tail -3 gpurun_out/r03_m2_tests.log
+timeout -k 10 240 python -u tools/convbench.py --blocks --variants 13 30 --mb 1024 --iters 10 --ablate 0 64 --shapes l3.c2+id l3.c2+ds l4.c2+id l4.c2+ds > gpurun_out/r03_m2_convbench.log 2>&1 || exit $?
+timeout -k 10 240 python -u tools/convbench.py --blocks --variants 30 --mb 1024 --iters 10 --shapes l4.c2+id l3.c2+id --ablate 1 16 32 80 96 > gpurun_out/r03_m2_ablate.log 2>&1 || exit $?
+cat gpurun_out/r03_m2_convbench.log gpurun_out/r03_m2_ablate.log
