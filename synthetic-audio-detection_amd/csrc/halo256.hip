@@ -52,6 +52,7 @@ constexpr int TW = 16, TH = 16, PW = TW + 2, PR = PW * (TH + 2);  // 18 x 18 pat
 constexpr int NDP = (PR + 7) / 8;  // 41 DMA pieces (8 pixel rows of 128 B) per patch chunk
 constexpr int NDS = BP / 8;        // 32 pieces per shortcut chunk
 constexpr int QP = (NDP + 3) / 4;  // <= 11 per patch wave
+constexpr int QPE = (NDP + 7) / 8; // <= 6 per wave when all 8 waves issue the patch
 constexpr int QS = NDS / 4;        // 8 per patch wave
 constexpr int QW = BC / 8 / 4;     // 8 weight pieces per weight wave and step
 constexpr int WST = BC * 128;      // one weight stage
@@ -127,11 +128,28 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
     }
     return 9 * cinb + (s - 9 * nc0) * 128;
   };
+  // Default: waves 0-3 issue the weights (8 pieces each per step), waves 4-7
+  // the patch (taps 0-3 of a chunk) at the top of each step, ahead of the
+  // weight burst in the CU's DMA queue (issued after their half-0 MFMAs, ablate
+  // bit 64, they waited behind it: l4.c2 +5-15 %).  EVEN (ablate bit 128, A/B):
+  // every wave issues 4 weight pieces and at most one patch piece (taps 0-5),
+  // waves 4-7 after their half-0 MFMAs (bit 256: all waves after the reads):
+  // 8-12 % slower than the default, with ~1.8k cycles per step in the early
+  // waves' issue (stamps) for 5 pieces.
+  const bool even = (a.ablate & 128) != 0;
   auto issue_weights = [&](int kb, int stage) __attribute__((always_inline)) {
+    if (even) {
 #pragma unroll
-    for (int i = 0; i < QW; ++i) {
-      const int q = lw + 4 * i;
-      dma16_m0(rw, wlane + q * 8 * wrow + kb, lds0 + stage * WST + q * 1024);
+      for (int i = 0; i < QW / 2; ++i) {
+        const int q = wave + 8 * i;
+        dma16_m0(rw, wlane + q * 8 * wrow + kb, lds0 + stage * WST + q * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < QW; ++i) {
+        const int q = lw + 4 * i;
+        dma16_m0(rw, wlane + q * 8 * wrow + kb, lds0 + stage * WST + q * 1024);
+      }
     }
   };
 
@@ -147,8 +165,8 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   // made the patch waves' issue VALU-bound: l4.c2 1105 -> 932 us with the patch
   // DMA ablated.)
   auto patch_piece = [&](int yb, int xb, int base, int lr, int k, int buf) __attribute__((always_inline)) {
-    const int q = lw + 4 * k;
-    if (NDP % 4 == 0 || q < NDP) {
+    const int q = even ? wave + 8 * k : lw + 4 * k;
+    if (q < NDP) {
       const int pr = 8 * q + lr;
       const int py = pr / PW, px = pr - py * PW;
       const int iy = yb + py, ix = xb + px;
@@ -159,7 +177,7 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
     }
   };
   auto sc_piece = [&](int base, int k, int buf) __attribute__((always_inline)) {
-    const int q = lw + 4 * k;
+    const int q = even ? wave + 8 * k : lw + 4 * k;
     const int r = 8 * q + lrow, ty = r >> 4, tx = r & 15;
     dma16_m0(r1, base + (ty * a.W1 + tx) * (a.ss1 * ps1), lds0 + OFF_P + buf * PATCH + q * 1024);
   };
@@ -191,12 +209,13 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
       const int base = ((b * a.H + oy0 - 1) * a.W + ox0 - 1) * ps0 + x.c * 128 + sw16;
 #pragma unroll
       for (int k = 0; k < QP; ++k)
-        if (tap < 0 || k % 4 == tap) patch_piece(oy0 - 1, ox0 - 1, base, lr, k, buf);
+        if ((even ? k < QPE && (tap < 0 || k == tap) : (tap < 0 || k % 4 == tap)))
+          patch_piece(oy0 - 1, ox0 - 1, base, lr, k, buf);
     } else {
       const int base = ((b * a.H1 + oy0 * a.ss1) * a.W1 + ox0 * a.ss1) * ps1 + (x.c - nc0) * 128 + sw16;
 #pragma unroll
       for (int k = 0; k < QS; ++k)
-        if (tap < 0 || k % 4 == tap) sc_piece(base, k, buf);
+        if ((even ? k < QS / 2 : true) && (tap < 0 || k % 4 == tap)) sc_piece(base, k, buf);
     }
   };
 
@@ -206,10 +225,8 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
 
   // ---- prologue: weights of step 0, patch of the first chunk
   Chunk cur{tp_begin, 0};
-  if (wloader)
-    issue_weights(step_kb(0), 0);
-  else
-    issue_chunk(cur, 0, -1);
+  if (even || wloader) issue_weights(step_kb(0), 0);
+  if (even || !wloader) issue_chunk(cur, 0, -1);
 
   f32x4 acc[TC][TP];
 #pragma unroll
@@ -235,7 +252,8 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   };
   const int ab = a.ablate;  // timing ablations (wrong results): 1 no DMA in the loop, 2 no waits,
                             // 4 no barrier, 8 no epilogue, 16 no weight DMA, 32 no patch DMA;
-                            // 64: patch pieces at the step's top (same results)
+                            // 64: patch pieces after the half-0 MFMAs, 128: even issue,
+                            // 256: even issue without the stagger (same results)
   // weight fragment rows wc*128 + i*16 + fr: slot = chunk ^ (fr & 6)
   const int wsl0 = (fg ^ (fr & 6)) << 4, wsl1 = ((fg + 4) ^ (fr & 6)) << 4;
   const int wrow0 = (wc * 16 * TC + fr) * 128;
@@ -248,9 +266,8 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   auto compute = [&](int ws, int pbuf, auto prow, auto late) __attribute__((always_inline)) {
     const char* wb = smem + ws * WST + wrow0;
     const char* pb = smem + OFF_P + pbuf * PATCH;
-    // ablate bit 64 (A/B): the patch waves issue their pieces at the top of
-    // the step, ahead of the weight waves' burst in the CU's DMA queue
-    if (!wloader && (ab & 64) && !(ab & 33)) late();
+    // the patch waves' pieces at the top of the step (default; ablate bit 64: late)
+    if (!even && !wloader && !(ab & 64) && !(ab & 33)) late();
     __builtin_amdgcn_sched_barrier(0);
     uint4 wf[TC], pf[TP], pg[TP];
 #pragma unroll
@@ -260,7 +277,20 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
       const int r = prow(j);
       pf[j] = *(const uint4*)(pb + r * 128 + ((fg ^ (r & 6)) << 4));
     }
-    if (wloader && g + 1 < total && !(ab & 17)) issue_weights(kb_next, (g + 1) & 1);
+    // even: this step's patch piece (if any), then the next step's weights,
+    // both retired by the next top's vmcnt (the weights are the youngest);
+    // waves 0-3 issue here, their SIMD partners 4-7 after their half-0 MFMAs
+    // (ablate bit 256: all waves here), so one wave's DMA issue overlaps its
+    // partner's MFMAs
+    const bool dma_now = wloader || (ab & 256);
+    if (even) {
+      if (dma_now) {
+        if (!(ab & 33)) late();
+        if (g + 1 < total && !(ab & 17)) issue_weights(kb_next, (g + 1) & 1);
+      }
+    } else if (wloader && g + 1 < total && !(ab & 17)) {
+      issue_weights(kb_next, (g + 1) & 1);
+    }
     __builtin_amdgcn_sched_barrier(0);
     stamp(2);
 #pragma unroll
@@ -287,7 +317,11 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!wloader && !(ab & 97)) late();
+    if (even && !dma_now) {
+      if (!(ab & 33)) late();
+      if (g + 1 < total && !(ab & 17)) issue_weights(kb_next, (g + 1) & 1);
+    }
+    if (!even && !wloader && (ab & 64) && !(ab & 33)) late();
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (SR < TC) {
 #pragma unroll
@@ -386,7 +420,7 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   bool post_epi = false;
   auto top = [&](bool first_of_chunk) __attribute__((always_inline)) {
     stamp(0);
-    if ((wloader || first_of_chunk) && !(ab & 2)) {
+    if ((even || wloader || first_of_chunk) && !(ab & 2)) {
       if (post_epi)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
       else
@@ -394,52 +428,49 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
     }
     post_epi = false;
     if (!(ab & 4)) __builtin_amdgcn_s_barrier();
+    // compiler memory fence: LDS changed behind this barrier (without it, the
+    // unrolled taps' identical-address fragment loads would be merged across steps)
+    asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     stamp(1);
   };
 
-  // one runtime loop over the workgroup's K-steps (a fully unrolled 9-tap body
-  // let the compiler hoist every tap's fragment addresses and spill)
-  int t = tp_begin, c = 0, tap = 0;
-  Chunk nx = next_chunk(cur);
-  for (; g < total;) {
-    const bool sc = c >= nc0;  // shortcut chunk (1 step)
-    // K byte offset of the next step's weights (scalar, no division per step)
-    if (!sc && tap < 8)
-      kb_next = (tap + 1) * cinb + c * 128;
-    else if (c + 1 < nc0)
-      kb_next = (c + 1) * 128;
-    else if (c + 1 < nc0 + nk1)
-      kb_next = 9 * cinb + (c + 1 - nc0) * 128;
-    else
-      kb_next = 0;
-    top(tap == 0);
-    const int ky = tap / 3, kx = tap - 3 * (tap / 3);
-    const int rb = sc ? wp * TP * 16 + fr : (wp * TP + ky) * PW + kx + fr;  // fragment 0's pixel row
-    const int rs = sc ? 16 : PW;                                           // rows per tile row
-    const int pbuf = u & 1;
-    compute(
-        g & 1, pbuf, [&](int j) __attribute__((always_inline)) { return rb + j * rs; },
-        [&]() __attribute__((always_inline)) {
-          if (sc)
-            issue_chunk(nx, pbuf ^ 1, -1);
-          else if (tap < 4)
-            issue_chunk(nx, pbuf ^ 1, tap);
-        });
-    stamp(3);
-    ++g;
-    if (sc || ++tap == 9) {  // chunk done
-      tap = 0;
-      cur = nx;
-      nx = next_chunk(cur);
-      ++u;
-      if (++c == nc0 + nk1) {
-        if (!(ab & 8)) epilogue(t);
-        post_epi = true;
-        c = 0;
-        ++t;
+  // ---- the K loop, nested: tiles -> chunks (nc0 conv chunks of 9 taps, then
+  // nk1 shortcut chunks of 1 step) -> steps, with ONE inlined step body (two
+  // inlined copies, conv and shortcut, made the register allocator spill)
+  for (int t = tp_begin; t < tp_end; ++t) {
+    for (int c = 0; c < nc0 + nk1; ++c) {
+      const Chunk nx = next_chunk(Chunk{t, c});
+      const int pbuf = u & 1;
+      const bool sc = c >= nc0;
+      const int nsteps = sc ? 1 : 9;
+      // K byte offset of the first step of the next chunk (or next tile)
+      const int kb_chunk_next = c + 1 < nc0 ? (c + 1) * 128 : (c + 1 < nc0 + nk1 ? 9 * cinb + (c + 1 - nc0) * 128 : 0);
+      for (int tap = 0; tap < nsteps; ++tap) {
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        kb_next = tap + 1 < nsteps ? (tap + 1) * cinb + c * 128 : kb_chunk_next;
+        top(tap == 0);
+        // fragment 0's pixel row: conv tap (ky, kx) in the 18 x 18 patch, or the
+        // shortcut chunk's 16 x 16 rows; opaque, ordered after the barrier
+        int rb;
+        asm volatile("v_add_u32 %0, %1, %2" : "=v"(rb) : "v"(sc ? wp * TP * 16 + fr : wp * TP * PW + fr),
+                     "s"(sc ? 0 : ky * PW + kx));
+        const int rs = sc ? 16 : PW;
+        compute(
+            g & 1, pbuf, [&](int j) __attribute__((always_inline)) { return rb + j * rs; },
+            [&]() __attribute__((always_inline)) {
+              if (sc)
+                issue_chunk(nx, pbuf ^ 1, -1);
+              else if (tap < (even ? QPE : 4))
+                issue_chunk(nx, pbuf ^ 1, tap);
+            });
+        stamp(3);
+        ++g;
       }
+      ++u;
     }
+    if (!(ab & 8)) epilogue(t);
+    post_epi = true;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   SAD_CLOCK_STAMP(1);

@@ -919,7 +919,7 @@ extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_
     SAD_CHECK_HIP(hipGetLastError());
     rows = nb;
   }
-  SAD_REQUIRE(rows > 0 && rows <= kStatRowsMax, "statistic partial rows");
+  SAD_REQUIRE(rows > 0 && rows <= (fused ? kStatRowsMax : 1024), "statistic partial rows");
   hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(Cout), dim3(256), 0, s, ws, rows, P, Cout, gamma, beta, eps,
                      momentum, running_mean, running_var, stats);
   SAD_CHECK_HIP(hipGetLastError());

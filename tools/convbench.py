@@ -136,6 +136,8 @@ def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,), split=False):
                     continue
                 # the halo kernel (20) takes the identity shortcut as an epilogue residual
                 kw = dict(res=scx) if v in (20, 21, 25) else dict(sc=scx, sc_stride=2 if sc == 'ds' else 1)
+                if sc == 'id' and v == 13 and (v0 >> 8) & 512 // 256:
+                    kw = dict(res=scx)  # ablate bit 512: the identity as the epilogue residual (RES)
 
                 def run(o=None):
                     return block_conv(x, w, bias, stride, 1, relu=True, variant=v0, out=o, split=split, **kw)

@@ -5,3 +5,5 @@ tail -3 gpurun_out/r03_m2_tests.log
 timeout -k 10 240 python -u tools/convbench.py --blocks --variants 13 30 --mb 1024 --iters 10 --ablate 0 64 --shapes l3.c2+id l3.c2+ds l4.c2+id l4.c2+ds > gpurun_out/r03_m2_convbench.log 2>&1 || exit $?
 timeout -k 10 240 python -u tools/convbench.py --blocks --variants 30 --mb 1024 --iters 10 --shapes l4.c2+id l3.c2+id --ablate 1 16 32 80 96 > gpurun_out/r03_m2_ablate.log 2>&1 || exit $?
 cat gpurun_out/r03_m2_convbench.log gpurun_out/r03_m2_ablate.log
+SAD_LIB=abl/libsad_stamps.so timeout -k 10 120 python -u tools/stamp_v30.py > gpurun_out/r03_m2_stamps.log 2>&1 || exit $?
+grep -v amdgpu.ids gpurun_out/r03_m2_stamps.log | grep -E "^---|stamps" | grep -A2 "v30"
