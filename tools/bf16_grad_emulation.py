@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Where the bf16 Bottleneck trainer's gradient error comes from (VERDICT r2
+item 6).  CPU autograd emulation: the reference's train-mode resnet50 step
+(oracle/train.py: CE on the pooled features, quirk C1; layer4 trainable) with
+every Conv2d / BatchNorm2d / ReLU output rounded to bf16 in the forward
+(straight-through gradient), optionally only some of them, or the gradients
+rounded in the backward; layer4 gradient cosine per block against the plain
+fp32 step on the same 4 images.
+
+Measured (4 images from tests/golden/golden_frontend.npz, weights
+sad.weights seed 7, head seed 42):
+  forward activations bf16 (all)        layer4.2 0.924 / .1 0.709 / .0 0.650
+  backward gradients bf16 only           1.000 / 1.000 / 1.000
+  forward bf16 except layer4             0.923 / 0.708 / 0.650
+  conv outputs only / BN+ReLU only       0.944 / 0.775 / 0.721 ; 0.941 / 0.764 / 0.716
+The device's bf16 trainer measures 0.93 / 0.70 / 0.62 (test_gpu_train.py), i.e.
+the same as the emulation: the layer4 gradients of this model are that
+sensitive to a 2^-9 relative perturbation of layer1-3's activations, and keeping
+layer4 (or the BN-backward inputs, or the backward) in fp32 does not move them.
+Test infrastructure (imports oracle/): python tools/bf16_grad_emulation.py
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'synthetic-audio-detection_amd')]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+class RoundFwd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class RoundBwd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+def step(base, head, img, tg, fwd=False, bwd=False, skip=lambda name, mod: False):
+    from oracle import train as otr
+    m, _ = otr.build(base, head, model_name='resnet50')
+    m.train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.ReLU):
+            mod.inplace = False
+    for name, mod in m.base.named_modules():
+        if isinstance(mod, (torch.nn.Conv2d, torch.nn.ReLU, torch.nn.BatchNorm2d)) and not skip(name, mod):
+            def hook(_m, _i, out):
+                y = RoundFwd.apply(out) if fwd else out
+                return RoundBwd.apply(y) if bwd else y
+            mod.register_forward_hook(hook)
+    torch.nn.CrossEntropyLoss()(m(img), tg).backward()
+    return {n: p.grad.clone() for n, p in m.base.named_parameters() if n.startswith('layer4.')}
+
+
+def main():
+    from oracle import frontend as ofe
+    from sad import train as st
+    from sad import weights as sw
+    base = sw.backbone_state_dict(7, 'resnet50')
+    head = st.init_state_dict(42, 'resnet50')[1]
+    fx = np.load(os.path.join(ROOT, 'tests', 'golden', 'golden_frontend.npz'))
+    img = ofe.resize_bilinear(torch.from_numpy(fx['std_map']).unsqueeze(1), (512, 512)).repeat(1, 3, 1, 1)
+    tg = torch.tensor([0, 1, 1, 0])
+    g0 = step(base, head, img, tg)
+    rows = [('forward activations bf16', dict(fwd=True)), ('backward gradients bf16', dict(bwd=True)),
+            ('forward bf16 except layer4', dict(fwd=True, skip=lambda n, m: n.startswith('layer4'))),
+            ('conv outputs bf16 only', dict(fwd=True, skip=lambda n, m: not isinstance(m, torch.nn.Conv2d))),
+            ('BN/ReLU outputs bf16 only', dict(fwd=True, skip=lambda n, m: isinstance(m, torch.nn.Conv2d)))]
+    for tag, kw in rows:
+        g = step(base, head, img, tg, **kw)
+        cos = {}
+        for b in ('layer4.2', 'layer4.1', 'layer4.0'):
+            a = torch.cat([g[n].flatten() for n in sorted(g) if n.startswith(b)]).double()
+            r = torch.cat([g0[n].flatten() for n in sorted(g0) if n.startswith(b)]).double()
+            cos[b] = round(torch.nn.functional.cosine_similarity(a, r, dim=0).item(), 4)
+        print(f'{tag:30s} {cos}', flush=True)
+
+
+if __name__ == '__main__':
+    main()

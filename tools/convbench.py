@@ -136,7 +136,7 @@ def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,), split=False):
                     continue
                 # the halo kernel (20) takes the identity shortcut as an epilogue residual
                 kw = dict(res=scx) if v in (20, 21, 25) else dict(sc=scx, sc_stride=2 if sc == 'ds' else 1)
-                if sc == 'id' and v == 13 and (v0 >> 8) & 512 // 256:
+                if sc == 'id' and v == 13 and (v0 >> 8) & 512:
                     kw = dict(res=scx)  # ablate bit 512: the identity as the epilogue residual (RES)
 
                 def run(o=None):
@@ -146,16 +146,22 @@ def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,), split=False):
                 same = 'ref' if ref is None else ('same' if torch.equal(out, ref) else
                                                   f'DIFF {(out.float() - ref.float()).abs().max().item():.3g}')
                 ref = out.clone() if ref is None else ref
+                # steady state: warm-up launches, then 3 timed runs of `iters`
+                # back-to-back launches each (per-launch events with a sync between
+                # launches let the clock drop and gave ~6 % run-to-run noise)
+                for _ in range(3):
+                    run(out)
                 ts = []
-                for _ in range(iters):
+                for _ in range(3):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    run(out)
+                    for _ in range(iters):
+                        run(out)
                     e1.record()
                     torch.cuda.synchronize()
-                    ts.append(e0.elapsed_time(e1))
+                    ts.append(e0.elapsed_time(e1) / iters)
                 ts.sort()
-                t = ts[len(ts) // 2]
+                t = ts[1]
                 ex = f'  exec {3 * flop / t / 1e9:7.1f} TF/s' if split else ''
                 print(f'{name:9s} mb={mb:4d} v={v} ablate={v0 >> 8}: {t * 1e3:9.1f} us  {flop / t / 1e9:7.1f} TF/s{ex}  '
                       f'{same}', flush=True)
