@@ -49,29 +49,37 @@ namespace h256 {
 constexpr int WC = 2, WP = 4, TC = 8, TP = 4;
 constexpr int BC = 16 * TC * WC, BP = 16 * TP * WP;  // 256 channels x 256 pixels
 constexpr int TW = 16, TH = 16, PW = TW + 2, PR = PW * (TH + 2);  // 18 x 18 patch
-constexpr int NDP = (PR + 7) / 8;  // 41 DMA pieces (8 pixel rows of 128 B) per patch chunk
-constexpr int NDS = BP / 8;        // 32 pieces per shortcut chunk
+constexpr int NDP = (PR + 7) / 8;  // 41 DMA pieces (8 patch slots of 128 B) per conv chunk
+constexpr int SCR = PW * TH;       // a shortcut chunk: 16 x 16 pixels at slots ty * 18 + tx
+constexpr int NDS = SCR / 8;       // 36 pieces per shortcut chunk
 constexpr int QP = (NDP + 3) / 4;  // <= 11 per patch wave
-constexpr int QPE = (NDP + 7) / 8; // <= 6 per wave when all 8 waves issue the patch
-constexpr int QS = NDS / 4;        // 8 per patch wave
+constexpr int QS = NDS / 4;        // 9 per patch wave
 constexpr int QW = BC / 8 / 4;     // 8 weight pieces per weight wave and step
 constexpr int WST = BC * 128;      // one weight stage
 constexpr int PATCH = NDP * 1024;
+constexpr int ROWB = PW * 128;     // bytes per patch row (18 slots)
 constexpr int OFF_P = 2 * WST;
 constexpr int OFF_BIAS = OFF_P + 2 * PATCH;
 constexpr int OFF_POOL = OFF_BIAS + BC * 4;
 constexpr int SMEM = OFF_POOL + WP * BC * 4;
 constexpr int BAD = 0x7FFFFFF0;  // past num_records: the DMA loads zeros (padding)
+// Patch swizzle: chunk c of a slot in patch column px (0..17) lands in 16-B
+// slot c ^ key(px), key = 3-bit entries of KEY.  A fragment's 16 lanes read 16
+// consecutive columns kx..kx+15 of one patch row; this table (found by a
+// search over the ds_read_b128 lane groups) is conflict-free for kx = 0, 1, 2
+// and both K-halves, and it depends on the column only, so a fragment's address
+// moves by a constant 18 x 128 B per patch row: each lane needs 6 addresses
+// (kx x half) for the whole kernel, and a tap's 4 row fragments are immediate
+// offsets.  (The previous key, on the slot index, cost ~40 VALU per K-step in
+// per-fragment address arithmetic: SQ_INSTS_VALU +49 % over variant 13.)
+constexpr uint64_t KEY = 0xd92dad912240ull;  // {0,0,1,1,2,2,4,4,5,5,6,6,2,2,6,6,0,0}
 static_assert(SMEM <= 160 * 1024, "LDS budget");
 }  // namespace h256
 
-template <typename F, int... I>
-__device__ __forceinline__ void h256_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void h256_for(F&& f) {
-  h256_for_impl(f, std::make_integer_sequence<int, N>{});
+__device__ __forceinline__ int h256_key(int px) { return (int)((h256::KEY >> (3 * px)) & 7); }
+// byte offset of lane (fr, fg)'s half-h fragment at patch column kx + fr of a patch row
+__device__ __forceinline__ int h256_po(int kx, int h, int fr, int fg) {
+  return (kx + fr) * 128 + (((fg + 4 * h) ^ h256_key(kx + fr)) << 4);
 }
 
 // X3: split-bf16 parity mode (block.hip): [hi 32 | lo 32] per 128-B chunk,
@@ -113,77 +121,30 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   const int ps0 = (int)a.in0_pstride * 2, ps1 = (int)a.in1_pstride * 2;
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   const int lrow = lane >> 3;
-  // DMA pieces write 8 rows x 8 chunks lane-linearly; row r's chunk c lands in
-  // slot c ^ (r & 6) (the halo swizzle, conflict-free for 16 consecutive rows at
-  // any offset), and r & 6 = lrow & 6 for every piece (pieces start at 8-row bounds)
-  const int sw16 = ((lane & 7) ^ (lrow & 6)) * 16;
 
-  // ---- weight waves: step cursor of the next weight DMA (K byte offset)
+  // ---- weight waves: the 256 weight rows of a K-step; row r's chunk c in slot
+  // c ^ (r & 6) (conflict-free for the fragments' 16 consecutive rows), and
+  // r & 6 = lrow & 6 for every piece (pieces start at 8-row bounds)
   const int wrow = a.wt_ld * 2;
-  const int wlane = (c0 + lrow) * wrow + sw16;
-  auto step_kb = [&](int s) __attribute__((always_inline)) {  // step s of a tile
-    if (s < 9 * nc0) {
-      const int ch = s / 9, tap = s - 9 * ch;
-      return tap * cinb + ch * 128;
-    }
-    return 9 * cinb + (s - 9 * nc0) * 128;
-  };
-  // Default: waves 0-3 issue the weights (8 pieces each per step), waves 4-7
-  // the patch (taps 0-3 of a chunk) at the top of each step, ahead of the
-  // weight burst in the CU's DMA queue (issued after their half-0 MFMAs, ablate
-  // bit 64, they waited behind it: l4.c2 +5-15 %).  EVEN (ablate bit 128, A/B):
-  // every wave issues 4 weight pieces and at most one patch piece (taps 0-5),
-  // waves 4-7 after their half-0 MFMAs (bit 256: all waves after the reads):
-  // 8-12 % slower than the default, with ~1.8k cycles per step in the early
-  // waves' issue (stamps) for 5 pieces.
-  const bool even = (a.ablate & 128) != 0;
+  const int wlane = (c0 + lrow) * wrow + (((lane & 7) ^ (lrow & 6)) << 4);
   auto issue_weights = [&](int kb, int stage) __attribute__((always_inline)) {
-    if (even) {
 #pragma unroll
-      for (int i = 0; i < QW / 2; ++i) {
-        const int q = wave + 8 * i;
-        dma16_m0(rw, wlane + q * 8 * wrow + kb, lds0 + stage * WST + q * 1024);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < QW; ++i) {
-        const int q = lw + 4 * i;
-        dma16_m0(rw, wlane + q * 8 * wrow + kb, lds0 + stage * WST + q * 1024);
-      }
+    for (int i = 0; i < QW; ++i) {
+      const int q = lw + 4 * i;
+      dma16_m0(rw, wlane + q * 8 * wrow + kb, lds0 + stage * WST + q * 1024);
     }
   };
 
-  // ---- patch waves: pieces of a chunk (3x3 patch of chunk c, or shortcut chunk s) of tile t
+  // ---- patch waves: the pieces of a chunk (conv chunk: the 18 x 18 patch of
+  // 64 channels; shortcut chunk: the 16 x 16 gathered pixels at slots ty*18+tx)
   auto tile_origin = [&](int t, int& b, int& oy0, int& ox0) __attribute__((always_inline)) {
     b = t / tiles_img;
     const int rem = t - b * tiles_img;
     oy0 = (rem / tiles_x) * TH;
     ox0 = (rem - (rem / tiles_x) * tiles_x) * TW;
   };
-  // The tile origin is wave-uniform and computed once per chunk issue (scalar
-  // divisions); a piece then costs ~10 VALU.  (Recomputing the origin per piece
-  // made the patch waves' issue VALU-bound: l4.c2 1105 -> 932 us with the patch
-  // DMA ablated.)
-  auto patch_piece = [&](int yb, int xb, int base, int lr, int k, int buf) __attribute__((always_inline)) {
-    const int q = even ? wave + 8 * k : lw + 4 * k;
-    if (q < NDP) {
-      const int pr = 8 * q + lr;
-      const int py = pr / PW, px = pr - py * PW;
-      const int iy = yb + py, ix = xb + px;
-      const int off = (pr < PR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
-                          ? base + (py * a.W + px) * ps0
-                          : BAD;
-      dma16_m0(r0, off, lds0 + OFF_P + buf * PATCH + q * 1024);
-    }
-  };
-  auto sc_piece = [&](int base, int k, int buf) __attribute__((always_inline)) {
-    const int q = even ? wave + 8 * k : lw + 4 * k;
-    const int r = 8 * q + lrow, ty = r >> 4, tx = r & 15;
-    dma16_m0(r1, base + (ty * a.W1 + tx) * (a.ss1 * ps1), lds0 + OFF_P + buf * PATCH + q * 1024);
-  };
-  // chunk u of the workgroup's sequence (per tile: nc0 patch chunks, then nk1 shortcut chunks)
   struct Chunk {
-    int t, c;  // tile; channel chunk (c < nc0) or shortcut chunk nc0 + s
+    int t, c;  // tile; conv chunk (c < nc0) or shortcut chunk nc0 + s
   };
   auto next_chunk = [&](Chunk x) __attribute__((always_inline)) {
     if (++x.c == nc0 + nk1) {
@@ -192,7 +153,9 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
     }
     return x;
   };
-  // pieces k = tap, tap + 4, ... of chunk x (all of them when tap < 0) into buffer buf
+  // pieces k = tap, tap + 4, ... of chunk x (all of them when tap < 0) into
+  // buffer buf.  The tile origin is wave-uniform, computed once per call
+  // (recomputed per piece, the patch waves' issue was VALU-bound).
   auto issue_chunk = [&](Chunk x, int buf, int tap) __attribute__((always_inline)) {
     if (x.t >= tp_end) return;
     int b, oy0, ox0;
@@ -200,22 +163,39 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
     b = __builtin_amdgcn_readfirstlane(b);
     oy0 = __builtin_amdgcn_readfirstlane(oy0);
     ox0 = __builtin_amdgcn_readfirstlane(ox0);
-    // lane row through an opaque move: the compiler would otherwise hoist every
+    // lane slot through an opaque move: the compiler would otherwise hoist every
     // piece's (py, px) out of the K loop into registers and spill
     int lr;
     asm volatile("v_mov_b32 %0, %1" : "=v"(lr) : "v"(lrow));
+    const unsigned dst = lds0 + OFF_P + buf * PATCH;
     if (x.c < nc0) {
-      // patch row py, column px at input (oy0 - 1 + py, ox0 - 1 + px)
-      const int base = ((b * a.H + oy0 - 1) * a.W + ox0 - 1) * ps0 + x.c * 128 + sw16;
+      // slot py*18 + px holds input pixel (oy0 - 1 + py, ox0 - 1 + px)
+      const int base = ((b * a.H + oy0 - 1) * a.W + ox0 - 1) * ps0 + x.c * 128;
 #pragma unroll
-      for (int k = 0; k < QP; ++k)
-        if ((even ? k < QPE && (tap < 0 || k == tap) : (tap < 0 || k % 4 == tap)))
-          patch_piece(oy0 - 1, ox0 - 1, base, lr, k, buf);
+      for (int k = 0; k < QP; ++k) {
+        const int q = lw + 4 * k;
+        if ((tap < 0 || k % 4 == tap) && q < NDP) {
+          const int s = 8 * q + lr, py = s / PW, px = s - py * PW;
+          const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+          const int off = (s < PR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+                              ? base + (py * a.W + px) * ps0 + (((lane & 7) ^ h256_key(px)) << 4)
+                              : BAD;
+          dma16_m0(r0, off, dst + q * 1024);
+        }
+      }
     } else {
-      const int base = ((b * a.H1 + oy0 * a.ss1) * a.W1 + ox0 * a.ss1) * ps1 + (x.c - nc0) * 128 + sw16;
+      // slot ty*18 + tx (tx < 16) holds shortcut pixel ((oy0 + ty) ss1, (ox0 + tx) ss1)
+      const int base = ((b * a.H1 + oy0 * a.ss1) * a.W1 + ox0 * a.ss1) * ps1 + (x.c - nc0) * 128;
 #pragma unroll
-      for (int k = 0; k < QS; ++k)
-        if ((even ? k < QS / 2 : true) && (tap < 0 || k % 4 == tap)) sc_piece(base, k, buf);
+      for (int k = 0; k < QS; ++k) {
+        const int q = lw + 4 * k;
+        if (tap < 0 || k % 4 == tap) {
+          const int s = 8 * q + lr, ty = s / PW, tx = s - ty * PW;
+          const int off = tx < TW ? base + (ty * a.W1 + tx) * (a.ss1 * ps1) + (((lane & 7) ^ h256_key(tx)) << 4)
+                                  : BAD;
+          dma16_m0(r1, off, dst + q * 1024);
+        }
+      }
     }
   };
 
@@ -223,10 +203,11 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   float* s_bias = (float*)(smem + OFF_BIAS);
   if (tid < BC / 4) *(float4*)(smem + OFF_BIAS + 16 * tid) = *(const float4*)(a.bias + c0 + 4 * tid);
 
-  // ---- prologue: weights of step 0, patch of the first chunk
-  Chunk cur{tp_begin, 0};
-  if (even || wloader) issue_weights(step_kb(0), 0);
-  if (even || !wloader) issue_chunk(cur, 0, -1);
+  // ---- prologue: weights of step 0 (K offset 0), patch of the first chunk
+  if (wloader)
+    issue_weights(0, 0);
+  else
+    issue_chunk(Chunk{tp_begin, 0}, 0, -1);
 
   f32x4 acc[TC][TP];
 #pragma unroll
@@ -252,52 +233,41 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   };
   const int ab = a.ablate;  // timing ablations (wrong results): 1 no DMA in the loop, 2 no waits,
                             // 4 no barrier, 8 no epilogue, 16 no weight DMA, 32 no patch DMA;
-                            // 64: patch pieces after the half-0 MFMAs, 128: even issue,
-                            // 256: even issue without the stagger (same results)
+                            // 64: the patch pieces after the half-0 MFMAs, 128: the weight
+                            // pieces after the half-0 MFMAs (same results)
   // weight fragment rows wc*128 + i*16 + fr: slot = chunk ^ (fr & 6)
   const int wsl0 = (fg ^ (fr & 6)) << 4, wsl1 = ((fg + 4) ^ (fr & 6)) << 4;
   const int wrow0 = (wc * 16 * TC + fr) * 128;
 
   int kb_next = 0;  // K byte offset of the next step's weights (set by the loop)
-  // ---- one K-step: fragments from weight stage `ws` and pixel rows prow(j)
-  // of patch buffer `pb`; the weight waves issue the next step's weights after
-  // their half-0 fragment reads (overlapping their latency), the patch waves
-  // their pieces (`late`) after their half-0 MFMAs
-  auto compute = [&](int ws, int pbuf, auto prow, auto late) __attribute__((always_inline)) {
-    const char* wb = smem + ws * WST + wrow0;
-    const char* pb = smem + OFF_P + pbuf * PATCH;
-    // the patch waves' pieces at the top of the step (default; ablate bit 64: late)
-    if (!even && !wloader && !(ab & 64) && !(ab & 33)) late();
+  // ---- one K-step: weight fragments from stage `ws`; pixel fragment j of
+  // half h at patch row wp*4 + ky + j, column kx + fr of buffer pbuf.  The
+  // weight waves issue the next step's weights after their half-0 fragment
+  // reads (overlapping their latency); the patch waves' pieces (`late`) go at
+  // the top of the step, ahead of the weight burst in the CU's DMA queue
+  // (after their half-0 MFMAs they waited behind it: l4.c2 +5-15 %)
+  auto compute = [&](int ws, int pbuf, int ky, int kx, auto late) __attribute__((always_inline)) {
+    if (!wloader && !(ab & 64) && !(ab & 33)) late();
     __builtin_amdgcn_sched_barrier(0);
+    const char* wb = smem + ws * WST + wrow0;
+    const int pbase = OFF_P + pbuf * PATCH + (wp * TP + ky) * ROWB;  // uniform
+    // (computed per step, ~12 VALU: a select among 6 precomputed offsets
+    // became a lookup table in scratch)
+    const int o0 = h256_po(kx, 0, fr, fg), o1 = h256_po(kx, 1, fr, fg);
+    const char* pb0 = smem + pbase + o0;
+    const char* pb1 = smem + pbase + o1;
     uint4 wf[TC], pf[TP], pg[TP];
 #pragma unroll
     for (int i = 0; i < TC; ++i) wf[i] = *(const uint4*)(wb + i * 16 * 128 + wsl0);
 #pragma unroll
-    for (int j = 0; j < TP; ++j) {
-      const int r = prow(j);
-      pf[j] = *(const uint4*)(pb + r * 128 + ((fg ^ (r & 6)) << 4));
-    }
-    // even: this step's patch piece (if any), then the next step's weights,
-    // both retired by the next top's vmcnt (the weights are the youngest);
-    // waves 0-3 issue here, their SIMD partners 4-7 after their half-0 MFMAs
-    // (ablate bit 256: all waves here), so one wave's DMA issue overlaps its
-    // partner's MFMAs
-    const bool dma_now = wloader || (ab & 256);
-    if (even) {
-      if (dma_now) {
-        if (!(ab & 33)) late();
-        if (g + 1 < total && !(ab & 17)) issue_weights(kb_next, (g + 1) & 1);
-      }
-    } else if (wloader && g + 1 < total && !(ab & 17)) {
-      issue_weights(kb_next, (g + 1) & 1);
-    }
+    for (int j = 0; j < TP; ++j) pf[j] = *(const uint4*)(pb0 + j * ROWB);
+    if (wloader && g + 1 < total && !(ab & 17) && !(ab & 128)) issue_weights(kb_next, (g + 1) & 1);
     __builtin_amdgcn_sched_barrier(0);
     stamp(2);
 #pragma unroll
-    for (int j = 0; j < TP; ++j) {
-      const int r = prow(j);
-      pg[j] = *(const uint4*)(pb + r * 128 + (((fg + 4) ^ (r & 6)) << 4));
-    }
+    for (int j = 0; j < TP; ++j) pg[j] = *(const uint4*)(pb1 + j * ROWB);
+    // half 0: per weight row i its TP (X3: 2 TP) MFMAs, then the read of its
+    // half-1 fragment into the freed registers (rolling prefetch, as variant 13)
     constexpr int SR = X3 ? 2 : TC;
     auto half0_row = [&](int i) __attribute__((always_inline)) {
 #pragma unroll
@@ -317,11 +287,10 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (even && !dma_now) {
-      if (!(ab & 33)) late();
-      if (g + 1 < total && !(ab & 17)) issue_weights(kb_next, (g + 1) & 1);
-    }
-    if (!even && !wloader && (ab & 64) && !(ab & 33)) late();
+    if (!wloader && (ab & 64) && !(ab & 33)) late();
+    // ablate bit 128 (A/B): the weight waves issue after their half-0 MFMAs,
+    // so their DMA stall overlaps the patch waves' MFMAs
+    if (wloader && g + 1 < total && !(ab & 17) && (ab & 128)) issue_weights(kb_next, (g + 1) & 1);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (SR < TC) {
 #pragma unroll
@@ -420,7 +389,7 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
   bool post_epi = false;
   auto top = [&](bool first_of_chunk) __attribute__((always_inline)) {
     stamp(0);
-    if ((even || wloader || first_of_chunk) && !(ab & 2)) {
+    if ((wloader || first_of_chunk) && !(ab & 2)) {
       if (post_epi)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
       else
@@ -428,8 +397,8 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
     }
     post_epi = false;
     if (!(ab & 4)) __builtin_amdgcn_s_barrier();
-    // compiler memory fence: LDS changed behind this barrier (without it, the
-    // unrolled taps' identical-address fragment loads would be merged across steps)
+    // compiler memory fence: LDS changed behind this barrier (fragment loads
+    // from the same addresses must not be merged across steps)
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     stamp(1);
@@ -450,20 +419,13 @@ __global__ __launch_bounds__(512, 2) void halo256_kernel(BlockConvArgs a) {
         const int ky = tap / 3, kx = tap - 3 * ky;
         kb_next = tap + 1 < nsteps ? (tap + 1) * cinb + c * 128 : kb_chunk_next;
         top(tap == 0);
-        // fragment 0's pixel row: conv tap (ky, kx) in the 18 x 18 patch, or the
-        // shortcut chunk's 16 x 16 rows; opaque, ordered after the barrier
-        int rb;
-        asm volatile("v_add_u32 %0, %1, %2" : "=v"(rb) : "v"(sc ? wp * TP * 16 + fr : wp * TP * PW + fr),
-                     "s"(sc ? 0 : ky * PW + kx));
-        const int rs = sc ? 16 : PW;
-        compute(
-            g & 1, pbuf, [&](int j) __attribute__((always_inline)) { return rb + j * rs; },
-            [&]() __attribute__((always_inline)) {
-              if (sc)
-                issue_chunk(nx, pbuf ^ 1, -1);
-              else if (tap < (even ? QPE : 4))
-                issue_chunk(nx, pbuf ^ 1, tap);
-            });
+        // a shortcut chunk's pixels sit at the conv tap (0, 0) positions
+        compute(g & 1, pbuf, ky, kx, [&]() __attribute__((always_inline)) {
+          if (sc)
+            issue_chunk(nx, pbuf ^ 1, -1);
+          else if (tap < 4)
+            issue_chunk(nx, pbuf ^ 1, tap);
+        });
         stamp(3);
         ++g;
       }
