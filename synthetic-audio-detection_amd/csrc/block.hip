@@ -696,6 +696,7 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
 
 int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s, bool x3 = false);
 int launch_halo256(const BlockConvArgs& a, hipStream_t s, bool x3);
+int launch_halo256r(const BlockConvArgs& a, hipStream_t s);
 bool halo256_ok(const BlockConvArgs& a);
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s);
 int launch_halo_rw_x3(const BlockConvArgs& a, hipStream_t s);
@@ -750,15 +751,16 @@ static bool x3_rw() {
   return v;
 }
 // SAD_HALO256=1 runs layer3/4's stride-1 convs on the patch-resident variant
-// 30 instead of the implicit GEMM (variant 13) (A/B switch; off by default
-// until it measures faster)
-static bool halo256_on() {
-  static const bool v = [] {
+// 30 instead of the implicit GEMM (variant 13), =2 (bf16) on variant 31
+// (register-resident weights, one barrier per chunk) (A/B switch)
+static int halo256_mode() {
+  static const int v = [] {
     const char* e = getenv("SAD_HALO256");
-    return e ? atoi(e) != 0 : false;
+    return e ? atoi(e) : 0;
   }();
   return v;
 }
+static bool halo256_on() { return halo256_mode() != 0; }
 static int block_device_cus() {
   static int cus[64] = {};
   int dev = 0;
@@ -786,7 +788,7 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   // leave CUs idle (one workgroup per CU), so split the channel tile (variant
   // 15, 128x256).  Both keep the 256-pixel tile and the same K order, so the
   // results (incl. the fused average pool) do not depend on the choice.
-  if (halo256_on() && halo256_ok(a)) return 30;  // layer3/4 stride-1 convs: patch-resident 256 x 256
+  if (halo256_on() && halo256_ok(a)) return halo256_mode() == 2 ? 31 : 30;  // layer3/4 stride-1 convs
   if (a.Cout % 256 == 0)
     return a.res || (a.M + 255) / 256 * (a.Cout / 256) >= block_device_cus() ? 13 : 15;  // 13: residual epilogue
   return a.Cout % 128 == 0 ? c128_variant() : 9;
@@ -794,7 +796,7 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
 // pixel tile of the variants that can fuse the average pool (0: cannot)
 static int pool_tile(int v) {
   switch (v) {
-    case 13: case 14: case 15: case 30: return 256;
+    case 13: case 14: case 15: case 30: case 31: return 256;
     case 16: return 512;
   }
   return 0;
@@ -805,7 +807,7 @@ bool block_conv_can_pool(const BlockConvArgs& a, int dtype) {
 }
 static bool variant_fits(int v, int cout) {
   if (v == 26) return cout == 64;
-  if (v == 30) return cout % 256 == 0;
+  if (v == 30 || v == 31) return cout % 256 == 0;
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128, 128};
   if (v == 20 || v == 21) return cout % 64 == 0;
   if (v == 22) return cout % 128 == 0;
@@ -956,6 +958,10 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
 #else
     return launch_halo256(a, s, dtype == SAD_BF16X3);
 #endif
+  }
+  if (v == 31) {
+    SAD_REQUIRE(dtype == SAD_BF16 && halo256_ok(a_in), "variant 31: bf16 3x3/s1/p1, Cout % 256, 16 x 16 tiles");
+    return launch_halo256r(a, s);
   }
   if (dtype == SAD_BF16X3 && v == 26) {
     SAD_REQUIRE(halo_ok(a_in, dtype), "split-bf16 halo conv: 3x3/s1/p1, H, W % 16");

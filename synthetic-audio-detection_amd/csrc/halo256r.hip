@@ -1,0 +1,353 @@
+// halo256r.hip -- variant 31: patch-resident 256 x 256 block conv with the
+// weights streamed straight into registers (bf16, gfx950).
+//
+// Replaces the same timm BasicBlock halves as variants 13 / 30 (conv -> bn
+// [-> + shortcut] -> relu, inference_runner.py:49-51 via timm resnet18
+// forward_features) for the layer3 / layer4 convs with stride 1:
+//   out[px, co] = act( sum_{tap, ci} X0[px + tap; ci] W0[co, tap, ci]
+//                    + sum_{k1} X1[px * ss1; k1] W1[co, k1] + bias[co] )
+//
+// Why a third form.  Variants 13 and 30 stage BOTH operands in LDS and so need
+// a workgroup barrier per 64-deep K-step (the weight stage of step g+1 is
+// filled by DMA while step g reads the other one).  Their stamps put a K-step
+// at ~3,600 cycles for 2,048 cycles of MFMA per SIMD: after every barrier both
+// waves of a SIMD read fragments and issue DMA at the same time, so the matrix
+// pipe idles ~1,000 cycles per step, and a DMA burst stalls the issuing wave.
+// Here each of the 8 waves owns 32 output channels x all 256 pixels of the
+// 16 x 16 tile:
+//  * its weight fragments (2 channel tiles x 2 K-halves, 16 B per lane each)
+//    are read from global memory (L2) straight into VGPRs, one K-step ahead,
+//    with a counted wait -- no LDS, no barrier, no redundancy (the waves own
+//    disjoint channels);
+//  * the pixel operand is the 18 x 18 input patch of a 64-channel chunk in LDS
+//    (variant 30's column-keyed swizzle: a fragment is a lane constant + an
+//    immediate row offset), DMA'd during the previous chunk, one piece per
+//    wave per tap;
+//  * so the only barrier is per chunk (every 9 K-steps): within a chunk the
+//    two waves of a SIMD drift freely and one's fragment reads overlap the
+//    other's MFMAs.
+// Per K-step and wave: 4 x 16-B weight loads, 32 ds_read_b128 (LDS ~50 % busy
+// at the MFMA rate), 64 MFMA 16x16x32.  Accumulators 128 VGPRs (2 x 16 tiles).
+// Epilogue: register-only (bias, ReLU, bf16, 8-B stores) or the fused average
+// pool (a wave holds all 256 pixels of its channels: no cross-wave reduction).
+#include "common.hpp"
+#include "igemm.hpp"
+#include "kernels.hpp"
+
+namespace sad {
+
+namespace h31 {
+constexpr int NW = 8, TC = 2, TP = 16;  // waves; per wave 2 x 16 channels x 16 x 16 pixels
+constexpr int BC = 16 * TC * NW;        // 256 channels per workgroup
+constexpr int TW = 16, TH = 16, PW = TW + 2, PR = PW * (TH + 2);
+constexpr int NDP = (PR + 7) / 8;       // 41 pieces per conv chunk
+constexpr int SCR = PW * TH;            // shortcut chunk: slots ty * 18 + tx
+constexpr int NDS = SCR / 8;            // 36 pieces per shortcut chunk
+constexpr int PATCH = NDP * 1024;
+constexpr int ROWB = PW * 128;
+constexpr int OFF_BIAS = 2 * PATCH;
+constexpr int SMEM = OFF_BIAS + BC * 4;
+constexpr int BAD = 0x7FFFFFF0;
+constexpr uint64_t KEY = 0xd92dad912240ull;  // variant 30's column key {0,0,1,1,2,2,4,4,5,5,6,6,2,2,6,6,0,0}
+static_assert(SMEM <= 160 * 1024, "LDS budget");
+}  // namespace h31
+
+__device__ __forceinline__ int h31_key(int px) { return (int)((h31::KEY >> (3 * px)) & 7); }
+
+// 16 B per lane from buffer offset voff straight into VGPRs, not tracked by the
+// compiler's wait insertion (the kernel counts vmcnt itself)
+typedef unsigned int h31_v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ h31_v4 h31_load16(__amdgpu_buffer_rsrc_t rsrc, int voff) {
+  h31_v4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rsrc) : "memory");
+  return v;
+}
+
+template <bool POOL>
+__global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
+  using namespace h31;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int n_tc = a.Cout / BC;
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int tc = w % n_tc;  // both channel tiles of a pixel range share an XCD
+  const int gp = gridDim.x / n_tc, wi = w / n_tc;
+  const int tiles_x = a.W / TW, tiles_img = tiles_x * (a.H / TH);
+  const int tiles_p = a.N * tiles_img;
+  const int tp_begin = (int)((int64_t)wi * tiles_p / gp), tp_end = (int)((int64_t)(wi + 1) * tiles_p / gp);
+  const int c0 = tc * BC;
+  if (tp_begin >= tp_end) return;  // whole workgroup (uniform)
+  const int cw = c0 + wave * 16 * TC;  // this wave's first output channel
+
+  const int cinb = a.Cin * 2;
+  const int nc0 = cinb / 128;                    // conv chunks (9 taps each)
+  const int nk1 = a.in1 ? a.Cin1 * 2 / 128 : 0;  // shortcut chunks (1 step each)
+  const int nch = nc0 + nk1;
+
+  const __amdgpu_buffer_rsrc_t r0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.in1 ? a.in1 : a.in0), (short)0, (int)a.in1_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, (int)a.wt_bytes, 0x00020000);
+  const int ps0 = (int)a.in0_pstride * 2, ps1 = (int)a.in1_pstride * 2;
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const int lrow = lane >> 3;
+  const int ab = a.ablate;  // timing ablations (wrong results): 1 no loads / DMA in the loop, 8 no epilogue
+
+  // ---- weights: lane (fr, fg) of fragment (i, h) = row cw + i*16 + fr, K bytes
+  // kb + h*64 + fg*16 of the step (kb = tap * cinb + chunk * 128)
+  const int wrow = a.wt_ld * 2;
+  const int wlane = (cw + fr) * wrow + fg * 16;
+  auto load_w = [&](int kb, h31_v4 (&wv)[TC][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < TC; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) wv[i][h] = h31_load16(rw, wlane + i * 16 * wrow + kb + h * 64);
+  };
+  auto kb_of = [&](int c, int tap) __attribute__((always_inline)) {
+    return c < nc0 ? tap * cinb + c * 128 : 9 * cinb + (c - nc0) * 128;
+  };
+
+  // ---- patch pieces of chunk c of tile t into buffer buf: piece q = wave + 8k
+  // (k = -1: all of this wave's pieces); the tile origin is wave-uniform
+  auto issue_patch = [&](int t, int c, int buf, int k_only) __attribute__((always_inline)) {
+    if (t >= tp_end) return;
+    const int tt = __builtin_amdgcn_readfirstlane(t);
+    const int b = tt / tiles_img, rem = tt - b * tiles_img;
+    const int oy0 = (rem / tiles_x) * TH, ox0 = (rem - (rem / tiles_x) * tiles_x) * TW;
+    int lr;  // opaque lane row: keeps the per-piece (py, px) from being hoisted into registers
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lr) : "v"(lrow));
+    const unsigned dst = lds0 + buf * PATCH;
+    if (c < nc0) {
+      const int base = ((b * a.H + oy0 - 1) * a.W + ox0 - 1) * ps0 + c * 128;
+#pragma unroll
+      for (int k = 0; k < (NDP + NW - 1) / NW; ++k) {
+        const int q = wave + NW * k;
+        if ((k_only < 0 || k == k_only) && q < NDP) {
+          const int s = 8 * q + lr, py = s / PW, px = s - py * PW;
+          const int iy = oy0 - 1 + py, ix = ox0 - 1 + px;
+          const int off = (s < PR && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+                              ? base + (py * a.W + px) * ps0 + (((lane & 7) ^ h31_key(px)) << 4)
+                              : BAD;
+          dma16_m0(r0, off, dst + q * 1024);
+        }
+      }
+    } else {
+      const int base = ((b * a.H1 + oy0 * a.ss1) * a.W1 + ox0 * a.ss1) * ps1 + (c - nc0) * 128;
+#pragma unroll
+      for (int k = 0; k < (NDS + NW - 1) / NW; ++k) {
+        const int q = wave + NW * k;
+        if ((k_only < 0 || k == k_only) && q < NDS) {
+          const int s = 8 * q + lr, ty = s / PW, tx = s - ty * PW;
+          const int off = tx < TW ? base + (ty * a.W1 + tx) * (a.ss1 * ps1) + (((lane & 7) ^ h31_key(tx)) << 4)
+                                  : BAD;
+          dma16_m0(r1, off, dst + q * 1024);
+        }
+      }
+    }
+  };
+
+  // ---- bias into LDS; prologue loads: the first chunk's patch, step 0's weights
+  float* s_bias = (float*)(smem + OFF_BIAS);
+  if (tid < BC / 4) *(float4*)(smem + OFF_BIAS + 16 * tid) = *(const float4*)(a.bias + c0 + 4 * tid);
+  issue_patch(tp_begin, 0, 0, -1);
+  h31_v4 wcur[TC][2], wnxt[TC][2];
+  load_w(0, wcur);
+
+  f32x4 acc[TC][TP];
+#pragma unroll
+  for (int i = 0; i < TC; ++i)
+#pragma unroll
+    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // vmcnt after a tile's epilogue: its 8-B stores are younger than the next
+  // step's weights and may stay in flight
+  constexpr int NST = POOL ? 0 : TC * TP;
+  bool post_epi = false;
+  // wait for this step's weights and everything older (at a chunk start: the
+  // chunk's patch pieces).  Per step the next step's weights are issued first,
+  // then at most one patch piece for the NEXT chunk, which may stay in flight
+  // (pend = 1); after a tile's epilogue its stores may.  The "+v" operands
+  // order the wait before the weights' first use.
+  bool pend = false;
+  auto wait_w = [&]() __attribute__((always_inline)) {
+    if (post_epi)
+      asm volatile("s_waitcnt vmcnt(%4)"
+                   : "+v"(wcur[0][0]), "+v"(wcur[0][1]), "+v"(wcur[1][0]), "+v"(wcur[1][1])
+                   : "n"(NST)
+                   : "memory");
+    else if (pend)
+      asm volatile("s_waitcnt vmcnt(1)"
+                   : "+v"(wcur[0][0]), "+v"(wcur[0][1]), "+v"(wcur[1][0]), "+v"(wcur[1][1])::"memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)"
+                   : "+v"(wcur[0][0]), "+v"(wcur[0][1]), "+v"(wcur[1][0]), "+v"(wcur[1][1])::"memory");
+    post_epi = false;
+  };
+
+  // ---- one K-step: 64 MFMAs; the pixel fragment of output row j, half h is at
+  // patch row j + ky, column kx + fr (shortcut chunks: ky = kx = 0)
+  auto step = [&](int pbuf, int ky, int kx) __attribute__((always_inline)) {
+    const int pbase = pbuf * PATCH + ky * ROWB;
+    const int o0 = (kx + fr) * 128 + ((fg ^ h31_key(kx + fr)) << 4);
+    const int o1 = (kx + fr) * 128 + (((fg + 4) ^ h31_key(kx + fr)) << 4);
+    const char* pb0 = smem + pbase + o0;
+    const char* pb1 = smem + pbase + o1;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const char* pb = h ? pb1 : pb0;
+      uint4 bf[TP];
+#pragma unroll
+      for (int j = 0; j < TP; ++j) bf[j] = *(const uint4*)(pb + j * ROWB);
+#pragma unroll
+      for (int j = 0; j < TP; ++j)
+#pragma unroll
+        for (int i = 0; i < TC; ++i) mfma_chunk<u16>(__builtin_bit_cast(uint4, wcur[i][h]), bf[j], acc[i][j]);
+      // reads run 4 fragments ahead of the MFMAs that consume them
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+      for (int j = 0; j < TP - 4; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, TC, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * TC, 0);
+    }
+  };
+
+  auto epilogue = [&](int t) __attribute__((always_inline)) {
+    const int b = t / tiles_img, rem = t - b * tiles_img;
+    const int oy0 = (rem / tiles_x) * TH, ox0 = (rem - (rem / tiles_x) * tiles_x) * TW;
+    float4 bias[TC];
+#pragma unroll
+    for (int i = 0; i < TC; ++i) bias[i] = *(const float4*)(s_bias + (cw - c0) + i * 16 + fg * 4);
+    if constexpr (POOL) {
+      // the wave holds all 256 pixels of its channels: relu(acc + bias) summed
+      // over its 16 row fragments, then over the 16 lanes of a row (DPP)
+#pragma unroll
+      for (int i = 0; i < TC; ++i) {
+        const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
+        float ps[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = 0.f;
+#pragma unroll
+          for (int j = 0; j < TP; ++j) v += fmaxf(acc[i][j][r] + bb[r], 0.f);
+          ps[r] = row16_sum(v);
+        }
+        if (fr == 0)
+          *(float4*)(a.pool_out + (int64_t)b * a.Cout + cw + i * 16 + fg * 4) =
+              make_float4(ps[0] * (1.f / 256), ps[1] * (1.f / 256), ps[2] * (1.f / 256), ps[3] * (1.f / 256));
+      }
+    } else {
+      u16* __restrict__ out = (u16*)a.out;
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int64_t px = (int64_t)(b * a.H + oy0 + j) * a.W + ox0 + fr;
+#pragma unroll
+        for (int i = 0; i < TC; ++i) {
+          const int co = cw + i * 16 + fg * 4;
+          float v[4] = {acc[i][j][0] + bias[i].x, acc[i][j][1] + bias[i].y, acc[i][j][2] + bias[i].z,
+                        acc[i][j][3] + bias[i].w};
+          if (a.relu)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+          uint2 q;
+          q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *(uint2*)(out + px * a.out_pstride + co) = q;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TC; ++i)
+#pragma unroll
+      for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // ---- the K loop: tiles -> chunks -> steps.  Per step: wait for its weights;
+  // at a chunk start also the barrier that publishes the chunk's patch (and
+  // frees the other buffer); then this step's patch piece for the next chunk
+  // (conv taps 1..6: one piece per wave; a shortcut chunk: all of them), the
+  // next step's weights, and the MFMAs.
+  int u = 0;  // chunk counter (patch buffer parity)
+  for (int t = tp_begin; t < tp_end; ++t) {
+    for (int c = 0; c < nch; ++c) {
+      const bool sc = c >= nc0;
+      const int nsteps = sc ? 1 : 9;
+      const int nt = c + 1 < nch ? t : t + 1, ncn = c + 1 < nch ? c + 1 : 0;  // next chunk
+      const int pbuf = u & 1;
+      for (int tap = 0; tap < nsteps; ++tap) {
+        wait_w();
+        if (tap == 0) {
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");  // LDS changed behind the barrier
+        }
+        pend = false;
+        if (!(ab & 1)) {
+          // the next step's weights (after the last step: a harmless reload of
+          // step 0's, so the wait counts stay uniform)
+          const int kbn = tap + 1 < nsteps ? kb_of(c, tap + 1) : kb_of(ncn, 0);
+          load_w(kbn, wnxt);
+          if (sc) {
+            issue_patch(nt, ncn, pbuf ^ 1, -1);  // waited for at the next step (a chunk start)
+          } else if (tap >= 1 && tap <= 6) {
+            issue_patch(nt, ncn, pbuf ^ 1, tap - 1);
+            pend = nt < tp_end && wave + NW * (tap - 1) < NDP;
+          }
+        }
+        const int ky = sc ? 0 : tap / 3, kx = sc ? 0 : tap - 3 * (tap / 3);
+        step(pbuf, ky, kx);
+#pragma unroll
+        for (int i = 0; i < TC; ++i)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) wcur[i][h] = wnxt[i][h];
+      }
+      ++u;
+    }
+    if (!(ab & 8)) epilogue(t);
+    post_epi = true;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool POOL>
+static int launch_halo256r_t(const BlockConvArgs& a, hipStream_t s) {
+  using namespace h31;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)halo256r_kernel<POOL>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    attr = true;
+  }
+  const int n_tc = a.Cout / BC;
+  const int64_t tiles_p = (int64_t)a.N * (a.H / TH) * (a.W / TW);
+  int64_t g = std::min<int64_t>(tiles_p * n_tc, 256);
+  g = std::max<int64_t>(n_tc, g / n_tc * n_tc);
+  hipLaunchKernelGGL((halo256r_kernel<POOL>), dim3((unsigned)g), dim3(512), SMEM, s, a);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
+}
+
+// (a: the kernel's bf16 channel counts and strides, as launch_block_conv passes them)
+int launch_halo256r(const BlockConvArgs& a, hipStream_t s) {
+  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1, "variant 31: 3x3, stride 1, pad 1");
+  SAD_REQUIRE(!a.res && !a.st_part, "variant 31: no epilogue residual / fused statistics (shortcut as in1)");
+  SAD_REQUIRE(a.Cout % h31::BC == 0, "variant 31: Cout must be a multiple of 256");
+  SAD_REQUIRE(a.H % 16 == 0 && a.W % 16 == 0 && a.Ho == a.H && a.Wo == a.W, "variant 31: image must tile by 16 x 16");
+  SAD_REQUIRE((a.Cin * 2) % 128 == 0 && (!a.in1 || (a.Cin1 * 2) % 128 == 0), "variant 31: whole 128-B chunks");
+  SAD_REQUIRE(!a.in1 || ((a.Ho - 1) * a.ss1 < a.H1 && (a.Wo - 1) * a.ss1 < a.W1), "variant 31: shortcut source");
+  SAD_REQUIRE(a.wt_ld >= 9 * a.Cin + (a.in1 ? a.Cin1 : 0) && (a.wt_ld * 2) % 16 == 0, "variant 31: weight rows");
+  SAD_REQUIRE(a.out_pstride % 4 == 0 && a.in0_pstride % 8 == 0 && (!a.in1 || a.in1_pstride % 8 == 0),
+              "variant 31: pixel strides");
+  SAD_REQUIRE(a.out || a.pool_out, "null output");
+  SAD_REQUIRE(a.M == (int64_t)a.N * a.H * a.W, "variant 31: M = N H W");
+  if (a.pool_out) {
+    SAD_REQUIRE(a.H == 16 && a.W == 16, "variant 31 fused average pool: a 16 x 16 tile must be one image");
+    return launch_halo256r_t<true>(a, s);
+  }
+  return launch_halo256r_t<false>(a, s);
+}
+
+}  // namespace sad

@@ -62,15 +62,16 @@ CASES = [
     ('l3-id', 3, 14, 256, 256, 1, 'id', [13, 17, 10, 19]),
     ('l3-s2', 2, 18, 128, 256, 2, None, [13, 17, 19]),
     ('l4-ds', 5, 6, 512, 512, 1, 'ds', [13, 17, 19]),
-    # variant 30 (patch-resident 256 x 256, halo256.hip): chunk-outer K order, so
-    # its own cases; ragged tile counts per persistent workgroup (280 tiles on 256)
-    ('l3-plain-30', 3, 32, 256, 256, 1, None, [30]),
-    ('l3-plain-30-ragged', 70, 32, 256, 256, 1, None, [30]),
-    ('l3-id-30', 2, 32, 256, 256, 1, 'id', [30]),
-    ('l3-ds-30', 2, 16, 128, 256, 1, 'ds', [30]),
-    ('l4-ds-30', 3, 16, 256, 512, 1, 'ds', [30]),
-    ('l4-id-30', 5, 16, 512, 512, 1, 'id', [30]),
-    ('l4-plain-30-rect', 2, 32, 512, 512, 1, None, [30]),
+    # variants 30 / 31 (patch-resident 256 x 256, halo256.hip / halo256r.hip):
+    # chunk-outer K order, so their own cases, bit-identical to each other;
+    # ragged tile counts per persistent workgroup (280 tiles on 256)
+    ('l3-plain-30', 3, 32, 256, 256, 1, None, [30, 31]),
+    ('l3-plain-30-ragged', 70, 32, 256, 256, 1, None, [30, 31]),
+    ('l3-id-30', 2, 32, 256, 256, 1, 'id', [30, 31]),
+    ('l3-ds-30', 2, 16, 128, 256, 1, 'ds', [30, 31]),
+    ('l4-ds-30', 3, 16, 256, 512, 1, 'ds', [30, 31]),
+    ('l4-id-30', 5, 16, 512, 512, 1, 'id', [30, 31]),
+    ('l4-plain-30-rect', 2, 32, 512, 512, 1, None, [30, 31]),
 ]
 
 

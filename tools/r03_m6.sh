@@ -1,0 +1,7 @@
+set -o pipefail
+cd /root/repo; mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_blockconv.py tests/test_gpu_x3.py -k "30" > gpurun_out/r03_m6_tests.log 2>&1 || { tail -30 gpurun_out/r03_m6_tests.log; exit 1; }
+tail -1 gpurun_out/r03_m6_tests.log
+timeout -k 10 400 python -u tools/convbench.py --blocks --variants 13 30 --mb 1024 --iters 10 --ablate 0 128 --shapes l3.c2+id l3.c2+ds l4.c2+id l4.c2+ds > gpurun_out/r03_m6_convbench.log 2>&1 || exit $?
+cat gpurun_out/r03_m6_convbench.log | grep -v "v=13 ablate=128"
+bash tools/ab_env.sh "tree:SAD_HALO256=0 tree:SAD_HALO256=1" 3 2>&1 | tee gpurun_out/r03_m6_ab.log || exit 1
