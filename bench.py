@@ -19,7 +19,7 @@ configs[2]) it carries, measured in the same run on the same segments:
     against the fp32 device path over the whole batch, decision agreement;
   * ``accuracy``: the same numbers for the bf16 headline mode;
   * ``fp32_mode``: the f32-MFMA mode's rate (N = 1);
-  * ``roofline`` (the dominant kernel, the 256x256 block-conv of layer3/4:
+  * ``roofline`` (the dominant kernel, variant 31 of the layer3/4 stride-1 convs:
     algorithmic FLOPs of its launches in the last timed step over their HIP
     event durations recorded by libsad on the launch stream; ``traffic`` from
     the committed PMC passes) and ``cpu_baseline`` (configs[0]: the CPU oracle
@@ -47,10 +47,14 @@ BACKBONE_FLOP = 18.13e9        # ResNet-18 @512^2 with conv1's 3 identical chann
 BF16_PEAK_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3        # f32 MFMA = f32 vector peak (MI355X_MICROARCH.md)
 # The dominant kernel and its rocprof key in the committed PMC traffic file
-DOMINANT_VARIANT = 13
-DOMINANT_KERNEL = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1, false, false, false>|131072'
-DOMINANT_KERNEL_OLD = 'sad::block_conv_kernel<unsigned short, 2, 4, 8, 4, 2, 1, false>|131072'
-TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r02s3_pmc_traffic_final.json', 'r02_pmc_traffic.json', 'r01_pmc_traffic.json')
+# bf16: variant 31 (csrc/halo256r.hip), the 12 stride-1 layer3/4 convs of a
+# 2,048-segment step; the split-bf16 parity mode keeps variant 13 (all 16)
+DOMINANT_VARIANT = {'bf16': 31, 'bf16x3': 13, 'fp32': 13}
+DOMINANT_KERNEL = 'sad::halo256r_kernel<false>|131072'
+DOMINANT_DESC = ('sad::halo256r_kernel (variant 31): patch-resident 256-channel x 16x16-pixel conv, weights '
+                 'streamed into registers; the 12 stride-1 layer3/4 convs of a step (stride-2 convs stay on the '
+                 '256x256 implicit GEMM, variant 13)')
+TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r03_pmc_traffic.json', 'r02s3_pmc_traffic_final.json')
                      if os.path.exists(os.path.join(ROOT, 'profiles', f))), '')
 FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats
 FE_BYTES = 256000 + 128512     # int16 PCM read + fp32 [128, 251] map written
@@ -235,7 +239,7 @@ class Mode:
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         k_ms, k_n, k_fl = _lib.ctypes.c_double(), _lib.I64(), _lib.ctypes.c_double()
-        _lib.call('sad_profile_end', DOMINANT_VARIANT if profile else -1, _lib.ctypes.byref(k_ms),
+        _lib.call('sad_profile_end', DOMINANT_VARIANT[self.dtype] if profile else -1, _lib.ctypes.byref(k_ms),
                   _lib.ctypes.byref(k_n), _lib.ctypes.byref(k_fl))
         mean = lambda a, b: sum(e[a].elapsed_time(e[b]) for e in evs) / steps  # noqa: E731
         r = {'elapsed': elapsed, 'fe_ms': mean(0, 1), 'bb_ms': mean(1, 2), 'heads_ms': mean(2, 3),
@@ -355,7 +359,7 @@ def main():
         traffic = None
         if TRAFFIC_JSON and args.dtype == 'bf16':
             tr = json.load(open(TRAFFIC_JSON))
-            rec = tr.get(DOMINANT_KERNEL) or tr.get(DOMINANT_KERNEL_OLD)
+            rec = tr.get(DOMINANT_KERNEL)
             if rec and rec.get('hbm_read_bytes') is not None:
                 traffic = rec['hbm_read_bytes'] + rec['hbm_write_bytes']
         bb_alg = BACKBONE_FLOP * B / (r['bb_ms'] * 1e-3) / 1e12
@@ -372,8 +376,7 @@ def main():
                        'micro_batch': head.mb, 'parallelism': f'dp{world}',
                        'per_rank_ms_per_step': r['rank_ms_per_step'], 'per_rank_allgather_ms': r['rank_gather_ms']},
             'roofline': {'bound': 'mfma',
-                         'kernel': 'sad::block_conv_kernel 256x256 tile (variant 13): the layer3 + layer4 convs, '
-                                   '8 launches per micro-batch, about 35% of the bf16 step',
+                         'kernel': DOMINANT_DESC,
                          'achieved': round(exe, 1), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(exe / peak, 4),
                          'traffic': traffic, 'traffic_unit': 'memory-side bytes per launch = L2-miss traffic, Infinity-Cache hits '
                                                              'included (FETCH_SIZE x2 + WRITE_SIZE, '

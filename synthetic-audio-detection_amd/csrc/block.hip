@@ -750,17 +750,18 @@ static bool x3_rw() {
   }();
   return v;
 }
-// SAD_HALO256=1 runs layer3/4's stride-1 convs on the patch-resident variant
-// 30 instead of the implicit GEMM (variant 13), =2 (bf16) on variant 31
-// (register-resident weights, one barrier per chunk) (A/B switch)
+// The stride-1 3x3 convs with Cout % 256 == 0 (layer3/4): bf16 runs the
+// patch-resident variant 31 (weights streamed into registers, one barrier per
+// 64-channel chunk; 6-10 % faster than variant 13 per launch, +3 % end to end
+// same-box), split-bf16 the implicit GEMM (variant 13).  SAD_HALO256 (A/B
+// switch): 0 = variant 13 for both, 1 = variant 30 for both, 2 = the default.
 static int halo256_mode() {
   static const int v = [] {
     const char* e = getenv("SAD_HALO256");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }
-static bool halo256_on() { return halo256_mode() != 0; }
 static int block_device_cus() {
   static int cus[64] = {};
   int dev = 0;
@@ -778,7 +779,7 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   if (dtype == SAD_BF16X3) {
     // layer1 (64 -> 64): the resident-weight split-bf16 kernel (half the channels per workgroup)
     if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64 && x3_rw()) return 26;
-    if (halo256_on() && halo256_ok(a)) return 30;
+    if (halo256_mode() == 1 && halo256_ok(a)) return 30;
     return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   }
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
@@ -788,7 +789,10 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   // leave CUs idle (one workgroup per CU), so split the channel tile (variant
   // 15, 128x256).  Both keep the 256-pixel tile and the same K order, so the
   // results (incl. the fused average pool) do not depend on the choice.
-  if (halo256_on() && halo256_ok(a)) return halo256_mode() == 2 ? 31 : 30;  // layer3/4 stride-1 convs
+  // layer3/4 stride-1 convs (persistent, one 256-channel x 16 x 16 tile per
+  // workgroup: only when the tiles cover the CUs, else variant 15 below)
+  if (halo256_mode() != 0 && halo256_ok(a) && a.M / 256 * (a.Cout / 256) >= block_device_cus())
+    return halo256_mode() == 2 ? 31 : 30;
   if (a.Cout % 256 == 0)
     return a.res || (a.M + 255) / 256 * (a.Cout / 256) >= block_device_cus() ? 13 : 15;  // 13: residual epilogue
   return a.Cout % 128 == 0 ? c128_variant() : 9;

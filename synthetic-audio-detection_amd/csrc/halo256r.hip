@@ -54,14 +54,7 @@ static_assert(SMEM <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ int h31_key(int px) { return (int)((h31::KEY >> (3 * px)) & 7); }
 
-// 16 B per lane from buffer offset voff straight into VGPRs, not tracked by the
-// compiler's wait insertion (the kernel counts vmcnt itself)
 typedef unsigned int h31_v4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ h31_v4 h31_load16(__amdgpu_buffer_rsrc_t rsrc, int voff) {
-  h31_v4 v;
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rsrc) : "memory");
-  return v;
-}
 
 template <bool POOL>
 __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
@@ -105,7 +98,8 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
 #pragma unroll
     for (int i = 0; i < TC; ++i)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) wv[i][h] = h31_load16(rw, wlane + i * 16 * wrow + kb + h * 64);
+      for (int h = 0; h < 2; ++h)
+        wv[i][h] = __builtin_amdgcn_raw_buffer_load_b128(rw, wlane + i * 16 * wrow + kb + h * 64, 0, 0);
   };
   auto kb_of = [&](int c, int tap) __attribute__((always_inline)) {
     return c < nc0 ? tap * cinb + c * 128 : 9 * cinb + (c - nc0) * 128;
@@ -154,8 +148,10 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   float* s_bias = (float*)(smem + OFF_BIAS);
   if (tid < BC / 4) *(float4*)(smem + OFF_BIAS + 16 * tid) = *(const float4*)(a.bias + c0 + 4 * tid);
   issue_patch(tp_begin, 0, 0, -1);
+  // wnxt: the weights in flight (loaded one step ahead); wcur: this step's,
+  // copied from wnxt only after the step's wait
   h31_v4 wcur[TC][2], wnxt[TC][2];
-  load_w(0, wcur);
+  load_w(0, wnxt);
 
   f32x4 acc[TC][TP];
 #pragma unroll
@@ -163,29 +159,17 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // vmcnt after a tile's epilogue: its 8-B stores are younger than the next
-  // step's weights and may stay in flight
-  constexpr int NST = POOL ? 0 : TC * TP;
-  bool post_epi = false;
-  // wait for this step's weights and everything older (at a chunk start: the
-  // chunk's patch pieces).  Per step the next step's weights are issued first,
-  // then at most one patch piece for the NEXT chunk, which may stay in flight
-  // (pend = 1); after a tile's epilogue its stores may.  The "+v" operands
-  // order the wait before the weights' first use.
-  bool pend = false;
-  auto wait_w = [&]() __attribute__((always_inline)) {
-    if (post_epi)
-      asm volatile("s_waitcnt vmcnt(%4)"
-                   : "+v"(wcur[0][0]), "+v"(wcur[0][1]), "+v"(wcur[1][0]), "+v"(wcur[1][1])
-                   : "n"(NST)
-                   : "memory");
-    else if (pend)
-      asm volatile("s_waitcnt vmcnt(1)"
-                   : "+v"(wcur[0][0]), "+v"(wcur[0][1]), "+v"(wcur[1][0]), "+v"(wcur[1][1])::"memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)"
-                   : "+v"(wcur[0][0]), "+v"(wcur[0][1]), "+v"(wcur[1][0]), "+v"(wcur[1][1])::"memory");
-    post_epi = false;
+  // this step's weights: the copy from wnxt is where the compiler waits for
+  // the loads (weights are compiler-tracked buffer loads; the patch DMA pieces,
+  // inline asm, are not tracked, so each such wait also covers the pieces
+  // issued before it -- conservative, never short).  An inline-asm load with a
+  // hand-counted vmcnt gave wrong results: the register allocator may copy an
+  // asm output before the data has landed.
+  auto take_w = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < TC; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) wcur[i][h] = wnxt[i][h];
   };
 
   // ---- one K-step: 64 MFMAs; the pixel fragment of output row j, half h is at
@@ -273,6 +257,7 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   // (conv taps 1..6: one piece per wave; a shortcut chunk: all of them), the
   // next step's weights, and the MFMAs.
   int u = 0;  // chunk counter (patch buffer parity)
+  bool post_epi = false;
   for (int t = tp_begin; t < tp_end; ++t) {
     for (int c = 0; c < nch; ++c) {
       const bool sc = c >= nc0;
@@ -280,12 +265,18 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
       const int nt = c + 1 < nch ? t : t + 1, ncn = c + 1 < nch ? c + 1 : 0;  // next chunk
       const int pbuf = u & 1;
       for (int tap = 0; tap < nsteps; ++tap) {
-        wait_w();
         if (tap == 0) {
+          // the chunk's patch pieces (this wave's); after a tile's epilogue its
+          // stores (the youngest operations) may stay in flight
+          if (post_epi)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(POOL ? 0 : TC * TP) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          post_epi = false;
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");  // LDS changed behind the barrier
         }
-        pend = false;
+        take_w();
         if (!(ab & 1)) {
           // the next step's weights (after the last step: a harmless reload of
           // step 0's, so the wait counts stay uniform)
@@ -295,15 +286,10 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
             issue_patch(nt, ncn, pbuf ^ 1, -1);  // waited for at the next step (a chunk start)
           } else if (tap >= 1 && tap <= 6) {
             issue_patch(nt, ncn, pbuf ^ 1, tap - 1);
-            pend = nt < tp_end && wave + NW * (tap - 1) < NDP;
           }
         }
         const int ky = sc ? 0 : tap / 3, kx = sc ? 0 : tap - 3 * (tap / 3);
         step(pbuf, ky, kx);
-#pragma unroll
-        for (int i = 0; i < TC; ++i)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) wcur[i][h] = wnxt[i][h];
       }
       ++u;
     }
