@@ -291,6 +291,20 @@ int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t W, int32_t
                        int32_t stride, int32_t pad, int32_t relu, int32_t dtype, int32_t variant,
                        void* stream);
 
+/* One whole layer1 BasicBlock (timm resnet18 layer1.{0,1} with BN folded:
+ * out = relu(conv3x3(relu(conv3x3(x; w1) + b1); w2) + b2 + x), 64 channels,
+ * stride 1) as ONE fused kernel (csrc/l1block.hip, variant 40): the
+ * intermediate stays in LDS and the identity comes from the input patch.
+ * Replaces the two sad_block_conv_run launches (conv1; conv2 + res) of a
+ * layer1 block -- reference inference_runner.py:49-51 (timm forward_features).
+ * bf16 only.  x, out: NHWC [N,H,W,64] bf16 (must not overlap), H and W
+ * multiples of 16; w1, w2: [64][w_ld] bf16, k = tap * 64 + ci; b1, b2: [64]
+ * fp32.  ablate: 0 (timing-only bits otherwise, results wrong).  Async on
+ * `stream`. */
+int sad_l1_block_run(const void* x, int64_t N, int32_t H, int32_t W, const void* w1, int32_t w1_ld,
+                     const float* b1, const void* w2, int32_t w2_ld, const float* b2, void* out,
+                     int32_t ablate, void* stream);
+
 /* --------------------------------------------------------------- training */
 /* The submodel_trainer.py hot path: the train-mode
  * front end of SpectrogramDataset.__getitem__ (:139-214, transforms :463-471),

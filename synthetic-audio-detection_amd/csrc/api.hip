@@ -328,6 +328,28 @@ static int timed_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, do
   return rc;
 }
 
+// SAD_L1_FUSED=1 runs layer1's blocks on the fused BasicBlock kernel (variant
+// 40) instead of two convs per block (variant 25; A/B switch, off until faster)
+static bool l1_fused() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_L1_FUSED");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return v;
+}
+static int timed_l1block(const L1BlockArgs& a, hipStream_t s, double flops) {
+  if (!g_prof_on) return launch_l1block(a, s);
+  ProfRec r{40, flops, nullptr, nullptr};
+  SAD_CHECK_HIP(hipEventCreate(&r.e0));
+  SAD_CHECK_HIP(hipEventCreate(&r.e1));
+  SAD_CHECK_HIP(hipEventRecord(r.e0, s));
+  int rc = launch_l1block(a, s);
+  SAD_CHECK_HIP(hipEventRecord(r.e1, s));
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof.push_back(r);
+  return rc;
+}
+
 extern "C" int sad_profile_begin(void) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
   for (auto& r : g_prof) {
@@ -394,6 +416,24 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
     for (size_t bi = b0; bi < b1; ++bi) {
       const DevBlock& blk = p->blocks[bi];
       const int Ho = H / blk.stride;
+      if (p->dtype == SAD_BF16 && blk.stride == 1 && blk.cout == 64 && C == 64 && blk.cin == 64 && H % 16 == 0 &&
+          l1_fused()) {
+        // layer1: the whole BasicBlock as one kernel (variant 40)
+        L1BlockArgs f{};
+        f.x = (const u16*)bufA;
+        f.out = (u16*)bufB;
+        f.N = (int)mb;
+        f.H = f.W = H;
+        f.w1 = (const u16*)blk.w1;
+        f.w1_ld = 9 * 64;
+        f.b1 = blk.b1;
+        f.w2 = (const u16*)blk.w2;
+        f.w2_ld = 9 * 64 + blk.cin_sc;  // (the identity's K columns are not read)
+        f.b2 = blk.b2;
+        if ((rc = timed_l1block(f, s, 2.0 * 2.0 * mb * H * H * 64 * 576.0))) return rc;
+        std::swap(bufA, bufB);
+        continue;
+      }
       BlockConvArgs a{};
       a.in0 = bufA;
       a.in0_pstride = C;
@@ -859,6 +899,30 @@ extern "C" int sad_conv2d_run(const void* in, int64_t N, int32_t H, int32_t W, i
   a.relu = relu;
   a.M = N * a.Ho * a.Wo;
   return launch_conv(a, dtype, (hipStream_t)stream, variant);
+}
+
+extern "C" int sad_l1_block_run(const void* x, int64_t N, int32_t H, int32_t W, const void* w1, int32_t w1_ld,
+                                const float* b1, const void* w2, int32_t w2_ld, const float* b2, void* out,
+                                int32_t ablate, void* stream) {
+  SAD_REQUIRE(x && w1 && b1 && w2 && b2 && out, "null tensor");
+  SAD_REQUIRE(N >= 0 && N < (1ll << 31) && H > 0 && W > 0, "bad shape");
+  const int64_t bytes = N * H * W * 128;
+  SAD_REQUIRE((const char*)out + bytes <= (const char*)x || (const char*)x + bytes <= (const char*)out,
+              "fused layer1 block: out must not overlap x");
+  L1BlockArgs a{};
+  a.x = (const u16*)x;
+  a.out = (u16*)out;
+  a.N = (int)N;
+  a.H = H;
+  a.W = W;
+  a.w1 = (const u16*)w1;
+  a.w1_ld = w1_ld;
+  a.b1 = b1;
+  a.w2 = (const u16*)w2;
+  a.w2_ld = w2_ld;
+  a.b2 = b2;
+  a.ablate = ablate;
+  return launch_l1block(a, (hipStream_t)stream);
 }
 
 extern "C" int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* in1,

@@ -791,7 +791,8 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   // results (incl. the fused average pool) do not depend on the choice.
   // layer3/4 stride-1 convs (persistent, one 256-channel x 16 x 16 tile per
   // workgroup: only when the tiles cover the CUs, else variant 15 below)
-  if (halo256_mode() != 0 && halo256_ok(a) && a.M / 256 * (a.Cout / 256) >= block_device_cus())
+  // (bf16 only: the fp32 parity path stays on the implicit GEMM)
+  if (dtype == SAD_BF16 && halo256_mode() != 0 && halo256_ok(a) && a.M / 256 * (a.Cout / 256) >= block_device_cus())
     return halo256_mode() == 2 ? 31 : 30;
   if (a.Cout % 256 == 0)
     return a.res || (a.M + 255) / 256 * (a.Cout / 256) >= block_device_cus() ? 13 : 15;  // 13: residual epilogue

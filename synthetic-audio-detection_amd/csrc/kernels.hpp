@@ -77,6 +77,23 @@ struct BlockConvArgs {
   int* st_rows;          // host out: rows written to st_part by the launch
 };
 
+// Fused layer1 BasicBlock (l1block.hip, variant 40): bf16 NHWC, 64 channels,
+// pixel stride 64; out = relu(conv(relu(conv(x; w1) + b1); w2) + b2 + x)
+struct L1BlockArgs {
+  const u16* x;          // [N, H, W, 64]
+  u16* out;              // [N, H, W, 64] (must not alias x)
+  int N, H, W;
+  const u16* w1;         // [64][w1_ld]: k = tap * 64 + ci (BN folded)
+  int w1_ld;
+  const float* b1;       // [64]
+  const u16* w2;
+  int w2_ld;
+  const float* b2;
+  int64_t x_bytes;       // set by launch_l1block
+  int ablate;            // timing ablations (wrong results): 1 no patch DMA in the loop, 8 no epilogues
+};
+int launch_l1block(const L1BlockArgs& a, hipStream_t s);
+
 struct StemArgs {
   const float* map;      // [B, mh, mw] standardised maps (bilinearly resized in-kernel), or
   const float* img;      // [B, 512, 512] fp32 image (one channel of the reference's 3 identical

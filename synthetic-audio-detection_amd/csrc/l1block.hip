@@ -1,0 +1,411 @@
+// l1block.hip -- fused layer1 BasicBlock (variant 40, bf16, gfx950).
+//
+// One timm BasicBlock of layer1 with its BatchNorms folded (the reference runs
+// timm resnet18's forward_features, inference_runner.py:49-51):
+//   mid = relu(conv3x3(x; W1) + b1)
+//   out = relu(conv3x3(mid; W2) + b2 + x)          Cin = Cout = 64, stride 1
+// as ONE kernel: the 64-channel intermediate never leaves LDS, and the
+// identity shortcut is read from the input patch the first conv already holds.
+// Per 16 x 16 output tile the HBM traffic is the 20 x 20 input patch (50 KB,
+// L2/MALL-shared halo) + the 32 KB output, against 41 + 32 + 41 + 32 + 32 KB for
+// the two unfused convs (variant 25).
+//
+// Work split: 4 waves, ONE per SIMD; wave w owns 32 output channels
+// (cg = w & 1) of both convs and half the pixels (pg = w >> 1).  A wave's
+// weights for both convs (2 channel tiles x 18 K-steps x 2 convs x 16 B per
+// lane = 288 registers) are loaded ONCE into registers, so the tile loop reads
+// only pixel fragments from LDS (one ds_read_b128 per two MFMAs: half the LDS
+// array's rate) and needs no weight traffic, no weight ring and no per-tap
+// barrier: two barriers per tile (intermediate published; intermediate and
+// patch free again).
+//
+// conv1 computes the 18 x 18 intermediate (1-pixel halo for conv2) as 21
+// fragments of 16 pixels: 18 row-aligned ones (row y, columns 0-15) and 3
+// "leftover" ones holding columns 16-17 (pixel (8m + fr/2, 16 + (fr & 1)) of
+// fragment m; the last has 4 live pixels).  Wave pg takes rows 9pg..9pg+8 and
+// leftovers pg and 2+pg (m = 3 is a duplicate of m = 2's row 17: harmless
+// identical writes).  The 1.31x conv1 MFMA work (21 vs 16 fragments) is the
+// price of the fusion; the block runs 1.16x the MFMA work of two plain convs.
+//
+// LDS (144 KB): 2 x input patch [20 x 20 pixels][128 B] (the next tile's patch
+// is DMA'd during this tile's conv1, one piece per K-step), the intermediate
+// [18 x 18][128 B] and the biases.  Swizzles (16-B chunk c of a pixel row):
+//  * intermediate row (y, x): position c ^ key(x)  -- variant 30's column key,
+//    conflict-free for row-aligned fragments at every tap column, so conv2's
+//    fragment address is a lane constant + an immediate row offset;
+//  * patch row (Y, X): position c ^ key(X) ^ 2 (Y & 3) -- the row term is
+//    uniform over an aligned fragment (an XOR with a scalar keeps it
+//    conflict-free) and spreads the leftover fragments' 4 rows per column
+//    over 4 positions (conflict-free too; exhaustive check in
+//    tests/test_l1block_layout.py).
+// Zero padding: patch pixels outside the image are DMA'd as zeros (offset
+// past num_records); intermediate pixels outside the image are written as 0
+// (conv2 pads the block's intermediate, not relu(b1)).
+#include "common.hpp"
+#include "igemm.hpp"
+#include "kernels.hpp"
+
+#include <utility>
+
+namespace sad {
+
+namespace l1b {
+constexpr int NW = 4;                      // waves: one per SIMD
+constexpr int PWD = 20, PR = PWD * PWD;    // input patch 20 x 20 (halo 2)
+constexpr int IWD = 18, IR = IWD * IWD;    // intermediate 18 x 18 (halo 1)
+constexpr int PATCH = PR * 128;            // 51,200 B
+constexpr int PROW = PWD * 128, IROW = IWD * 128;
+constexpr int OFF_I = 2 * PATCH;           // patches double-buffered
+constexpr int OFF_B = OFF_I + IR * 128;    // b1 [64], b2 [64] fp32
+constexpr int SMEM = OFF_B + 2 * 64 * 4;
+constexpr int NDP = PR / 8;                // 50 DMA pieces of 8 pixel rows
+constexpr int QP = (NDP + NW - 1) / NW;    // 13 per wave (waves 2, 3: 12)
+constexpr int NA = 9;                      // row-aligned conv1 fragments per wave
+constexpr int NF = NA + 2;                 // + 2 leftover fragments
+constexpr int NS = 18;                     // K-steps per conv: 9 taps x 2 halves of 32 channels
+constexpr int NU1 = NS * NF;               // conv1 (read, 2 MFMA) units per wave
+constexpr int NU2 = NS * 8;                // conv2 units per wave
+constexpr int DQ = 4;                      // fragment reads in flight ahead of their MFMAs
+constexpr int W2V = 8;                     // conv2 K-steps of channel tile 1 whose weights sit in VGPRs
+constexpr int BAD = 0x7FFFFFF0;
+constexpr uint64_t KEY = 0xd92dad912240ull;  // variant 30's column key (columns 18, 19: 0)
+static_assert(SMEM <= 160 * 1024, "LDS budget");
+static_assert(NDP % 2 == 0, "pieces");
+}  // namespace l1b
+
+__device__ __forceinline__ int l1b_key(int x) { return (int)((l1b::KEY >> (3 * x)) & 7); }
+
+// acc (AGPR) [+]= w (AGPR) . b (VGPR)
+typedef unsigned int l1b_v4 __attribute__((ext_vector_type(4)));
+typedef unsigned int l1b_v2 __attribute__((ext_vector_type(2)));
+// acc (VGPR) [+]= w (AGPR) . b (VGPR).  hipcc places MFMA A/B operands only
+// in VGPRs, and the 288 weight registers of both convs do not fit there next
+// to the accumulators: the weights live in AGPRs, the MFMA is inline asm.
+__device__ __forceinline__ void l1b_mfma_a0(f32x4& acc, const l1b_v4& w, const uint4& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "a"(w), "v"(__builtin_bit_cast(l1b_v4, b)));
+}
+__device__ __forceinline__ void l1b_mfma_a(f32x4& acc, const l1b_v4& w, const uint4& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(__builtin_bit_cast(l1b_v4, b)));
+}
+// the same with the weights in VGPRs (the AGPR file holds 256 of the 288)
+__device__ __forceinline__ void l1b_mfma_v0(f32x4& acc, const l1b_v4& w, const uint4& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(w), "v"(__builtin_bit_cast(l1b_v4, b)));
+}
+__device__ __forceinline__ void l1b_mfma_v(f32x4& acc, const l1b_v4& w, const uint4& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "v"(__builtin_bit_cast(l1b_v4, b)));
+}
+// two floats -> packed bf16 pair (RNE), one v_cvt_pk_bf16_f32
+typedef __bf16 l1b_bf2 __attribute__((ext_vector_type(2)));
+typedef float l1b_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t l1b_pk(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((l1b_f2){lo, hi}, l1b_bf2));
+}
+
+template <typename F, int... I>
+__device__ __forceinline__ void l1b_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void l1b_for(F&& f) {
+  l1b_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
+  using namespace l1b;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int cg = wave & 1, pg = wave >> 1;
+  const int cw = cg * 32;  // this wave's first channel (both convs)
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles_x = a.W / 16, tiles_img = tiles_x * (a.H / 16);
+  const int tiles_p = a.N * tiles_img;
+  const int tp_begin = (int)((int64_t)w * tiles_p / gridDim.x), tp_end = (int)((int64_t)(w + 1) * tiles_p / gridDim.x);
+  if (tp_begin >= tp_end) return;  // whole workgroup (uniform)
+
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ro =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)a.x_bytes, 0x00020000);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const int ab = a.ablate;  // timing ablations (wrong results): 1 no patch DMA in the loop, 8 no epilogues
+
+  // ---- patch piece k of this wave (q = wave + 4k: rows 8q .. 8q+7): the
+  // lane's patch pixel (Y, X) and its source offset from the tile origin are
+  // tile-independent (computed once); a tile away from the image border needs
+  // no bounds test
+  int DREL[QP], DYX[QP];
+#pragma unroll
+  for (int k = 0; k < QP; ++k) {
+    const int r = 8 * (wave + NW * k) + (lane >> 3);
+    const int Y = (r * 205) >> 12, X = r - 20 * Y;  // r / 20 exactly for r < 400
+    const int c = (lane & 7) ^ l1b_key(X) ^ ((Y & 3) << 1);
+    DREL[k] = ((Y - 2) * a.W + (X - 2)) * 128 + (c << 4);
+    DYX[k] = Y | (X << 16);
+  }
+  // tile t's origin: image byte offset, (oy0, ox0), interior flag (uniform)
+  struct TileO {
+    int base, oy0, ox0;
+    bool inner;
+  };
+  auto tile_o = [&](int t) __attribute__((always_inline)) {
+    const int b = t / tiles_img, rem = t - b * tiles_img;
+    const int ty = rem / tiles_x;
+    TileO o;
+    o.oy0 = ty * 16;
+    o.ox0 = (rem - ty * tiles_x) * 16;
+    o.base = ((b * a.H + o.oy0) * a.W + o.ox0) * 128;
+    o.inner = o.oy0 >= 2 && o.oy0 + 18 <= a.H && o.ox0 >= 2 && o.ox0 + 18 <= a.W;
+    return o;
+  };
+  auto issue_piece = [&](int k, const TileO& o, int buf) __attribute__((always_inline)) {
+    if (wave + NW * k >= NDP) return;  // uniform
+    int off = o.base + DREL[k];
+    if (!o.inner) {
+      const int Y = DYX[k] & 0xFFFF, X = DYX[k] >> 16;
+      if (!((unsigned)(o.oy0 - 2 + Y) < (unsigned)a.H && (unsigned)(o.ox0 - 2 + X) < (unsigned)a.W)) off = BAD;
+    }
+    dma16_m0(rx, off, lds0 + buf * PATCH + (wave + NW * k) * 1024);
+  };
+
+  // ---- weights of both convs into registers: lane (fr, fg) of K-step s =
+  // (tap, h) holds channels (fg + 4h) * 8 .. +7 of tap `tap` for output
+  // channel cw + 16 i + fr
+  l1b_v4 w1r[2][NS];
+  l1b_v4 w2r[2][NS];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int tap = s >> 1, h = s & 1;
+      w1r[i][s] = *(const l1b_v4*)(a.w1 + (size_t)(cw + 16 * i + fr) * a.w1_ld + tap * 64 + (fg + 4 * h) * 8);
+      w2r[i][s] = *(const l1b_v4*)(a.w2 + (size_t)(cw + 16 * i + fr) * a.w2_ld + tap * 64 + (fg + 4 * h) * 8);
+    }
+  if (tid < 32) {
+    const float* src = tid < 16 ? a.b1 + 4 * tid : a.b2 + 4 * (tid - 16);
+    *(float4*)(smem + OFF_B + 16 * tid) = *(const float4*)src;
+  }
+#pragma unroll
+  for (int k = 0; k < QP; ++k) issue_piece(k, tile_o(tp_begin), 0);
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+
+  int pb = 0;
+  for (int t = tp_begin; t < tp_end; ++t) {
+    const bool has_next = t + 1 < tp_end;
+    const TileO onext = tile_o(has_next ? t + 1 : t);
+    const int b = t / tiles_img, rem = t - b * tiles_img;
+    const int ty = rem / tiles_x;
+    const int oy0 = ty * 16, ox0 = (rem - ty * tiles_x) * 16;
+    const int pbo = pb * PATCH;
+    const int pboa = pbo + pg * 9 * PROW;  // aligned fragments: rows 9pg + k
+    // Lane constants, derived per tile from an opaque copy of the lane id:
+    // the fragment addresses are tile-invariant, and hoisted out of the tile
+    // loop they would take registers next to the 288 of resident weights.
+    int ln;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    const int frt = ln & 15, fgt = ln >> 4, et = ln & 1;
+    // aligned fragment, patch column frt + kx: pixel row + chunk position of channel group fgt
+    int LAt[3], KXt[3], LYt[2], LR0t[2];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      LAt[kx] = (frt + kx) * 128 + ((fgt ^ l1b_key(frt + kx)) << 4);
+      KXt[kx] = fgt ^ l1b_key(16 + et + kx);
+    }
+    // leftover fragments l = 0, 1 (m = pg, 2 + pg): pixel (LYt, 16 + et)
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      const int m = l == 0 ? pg : 2 + pg;
+      LYt[l] = min(8 * m + (frt >> 1), IWD - 1);
+      LR0t[l] = (LYt[l] * PWD + 16 + et) * 128;
+    }
+
+    // ---------------- conv1: 18 x 18 intermediate ----------------
+    auto rd1 = [&](auto uc) __attribute__((always_inline)) -> uint4 {
+      constexpr int u = decltype(uc)::value;
+      constexpr int s = u / NF, k = u % NF;
+      constexpr int tap = s >> 1, h = s & 1, ky = tap / 3, kx = tap % 3;
+      if constexpr (k < NA) {
+        const int Y = 9 * pg + k + ky;                       // uniform
+        const int sg = ((Y & 3) << 5) ^ (h << 6);            // 2 (Y & 3) and the K-half, as chunk bits
+        return *(const uint4*)(smem + ((LAt[kx] ^ sg) + pboa) + (k + ky) * PROW);
+      } else {
+        constexpr int l = k - NA;
+        const int pos = KXt[kx] ^ (((LYt[l] + ky) & 3) << 1) ^ (h << 2);
+        return *(const uint4*)(smem + (LR0t[l] + pbo + (pos << 4)) + (ky * PWD + kx) * 128);
+      }
+    };
+    f32x4 acc[2][NF];
+    uint4 bq[DQ];
+    l1b_for<DQ>([&](auto uc) __attribute__((always_inline)) { bq[decltype(uc)::value] = rd1(uc); });
+    l1b_for<NU1>([&](auto uc) __attribute__((always_inline)) {
+      constexpr int u = decltype(uc)::value;
+      constexpr int s = u / NF, k = u % NF;
+      const uint4 bf = bq[u % DQ];
+      if constexpr (u + DQ < NU1) bq[u % DQ] = rd1(std::integral_constant<int, u + DQ>{});
+      if constexpr (k == 0 && s < QP)
+        if (has_next && !(ab & 1)) issue_piece(s, onext, pb ^ 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if constexpr (s == 0)
+          l1b_mfma_a0(acc[i][k], w1r[i][s], bf);
+        else
+          l1b_mfma_a(acc[i][k], w1r[i][s], bf);
+      }
+    });
+    // the asm MFMAs' results are read by compiler code next: 8-pass XDL write
+    // -> VALU read needs 12 wait states, which hipcc does not pad for asm
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 11" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- conv1 epilogue: relu(acc + b1) (0 outside the image) -> intermediate
+    if (!(ab & 8)) {
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        int y, x;
+        if (k < NA) {
+          y = 9 * pg + k;
+          x = frt;
+        } else {
+          y = LYt[k - NA];
+          x = 16 + et;
+        }
+        const bool in = (unsigned)(oy0 - 1 + y) < (unsigned)a.H && (unsigned)(ox0 - 1 + x) < (unsigned)a.W;
+        const uint32_t inm = in ? 0xFFFFFFFFu : 0u;  // (0 outside the image: conv2's zero padding)
+        const int p = y * IWD + x;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const float4 b4 = *(const float4*)(smem + OFF_B + (cw + 16 * i + fgt * 4) * 4);
+          const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[i][k][r] + bb[r], 0.f);
+          uint2 q;
+          q.x = l1b_pk(v[0], v[1]) & inm;
+          q.y = l1b_pk(v[2], v[3]) & inm;
+          const int c = (cw >> 3) + 2 * i + (fgt >> 1);
+          *(uint2*)(smem + OFF_I + p * 128 + ((c ^ l1b_key(x)) << 4) + (fgt & 1) * 8) = q;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    // ---------------- conv2 + identity ----------------
+    int ln2;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln2) : "v"(lane));
+    const int fr2 = ln2 & 15, fg2 = ln2 >> 4;
+    // conv2: intermediate fragments of output rows 8pg + jj
+    int I2[3][2];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        I2[kx][h] = OFF_I + pg * 8 * IROW + (((fr2 + kx) * 128 + ((fg2 ^ l1b_key(fr2 + kx)) << 4)) ^ (h << 6));
+    auto rd2 = [&](auto uc) __attribute__((always_inline)) -> uint4 {
+      constexpr int u = decltype(uc)::value;
+      constexpr int s = u / 8, jj = u % 8;
+      constexpr int tap = s >> 1, h = s & 1, ky = tap / 3, kx = tap % 3;
+      return *(const uint4*)(smem + I2[kx][h] + (jj + ky) * IROW);
+    };
+    f32x4 acc2[2][8];
+    l1b_for<DQ>([&](auto uc) __attribute__((always_inline)) { bq[decltype(uc)::value] = rd2(uc); });
+    l1b_for<NU2>([&](auto uc) __attribute__((always_inline)) {
+      constexpr int u = decltype(uc)::value;
+      constexpr int s = u / 8, jj = u % 8;
+      const uint4 bf = bq[u % DQ];
+      if constexpr (u + DQ < NU2) bq[u % DQ] = rd2(std::integral_constant<int, u + DQ>{});
+      l1b_for<2>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        // the last K-steps' weights of channel tile 1 sit in VGPRs
+        constexpr bool wv = i == 1 && s >= NS - W2V;
+        if constexpr (s == 0)
+          l1b_mfma_a0(acc2[i][jj], w2r[i][s], bf);
+        else if constexpr (wv)
+          l1b_mfma_v(acc2[i][jj], w2r[i][s], bf);
+        else
+          l1b_mfma_a(acc2[i][jj], w2r[i][s], bf);
+      });
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 11" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+
+    // this wave's patch pieces of the next tile have landed (they went out
+    // during conv1); the stores below may stay in flight
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ---- conv2 epilogue: relu(acc + b2 + x) -> out (8 B per lane)
+    if (!(ab & 8)) {
+      // residual (patch centre) of channels cw + 16 i + 4 fg2: pixel column fr2 + 2
+      int LRr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        LRr[i] = (fr2 + 2) * 128 + ((((cw >> 3) + 2 * i + (fg2 >> 1)) ^ l1b_key(fr2 + 2)) << 4) + (fg2 & 1) * 8;
+      const int obase = ((b * a.H + oy0 + 8 * pg) * a.W + ox0) * 128;  // uniform
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const uint2 rv = *(const uint2*)(smem + ((LRr[i] ^ ((((jj + 2) & 3)) << 5)) + pbo + pg * 8 * PROW) +
+                                           (jj + 2) * PROW);
+          const float4 b4 = *(const float4*)(smem + OFF_B + 256 + (cw + 16 * i + fg2 * 4) * 4);
+          const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+          float v[4];
+          v[0] = acc2[i][jj][0] + bb[0] + __uint_as_float(rv.x << 16);
+          v[1] = acc2[i][jj][1] + bb[1] + __uint_as_float(rv.x & 0xFFFF0000u);
+          v[2] = acc2[i][jj][2] + bb[2] + __uint_as_float(rv.y << 16);
+          v[3] = acc2[i][jj][3] + bb[3] + __uint_as_float(rv.y & 0xFFFF0000u);
+          uint2 q;
+          q.x = l1b_pk(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f));
+          q.y = l1b_pk(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(l1b_v2, q), ro, (jj * a.W + fr2) * 128 + (cw + 16 * i + 4 * fg2) * 2, obase, 0);
+        }
+      }
+    }
+    // the intermediate and patch pb are free, patch pb ^ 1 has landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    pb ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int launch_l1block(const L1BlockArgs& a_in, hipStream_t s) {
+  using namespace l1b;
+  SAD_REQUIRE(a_in.x && a_in.out && a_in.w1 && a_in.w2 && a_in.b1 && a_in.b2, "null tensor");
+  SAD_REQUIRE(a_in.N >= 0 && a_in.H % 16 == 0 && a_in.W % 16 == 0 && a_in.H > 0 && a_in.W > 0,
+              "fused layer1 block: H, W multiples of 16");
+  SAD_REQUIRE(a_in.w1_ld >= 576 && a_in.w2_ld >= 576 && a_in.w1_ld % 8 == 0 && a_in.w2_ld % 8 == 0,
+              "fused layer1 block: weight rows of >= 576 bf16, 16-B aligned");
+  if (a_in.N == 0) return SAD_OK;
+  static bool attr = false;
+  if (!attr) {
+    SAD_CHECK_HIP(hipFuncSetAttribute((const void*)l1block_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+    attr = true;
+  }
+  // the patch DMA addresses the input through 32-bit buffer offsets: split a
+  // batch past that range into image ranges (every image is independent)
+  const int64_t img = (int64_t)a_in.H * a_in.W * 128;
+  const int64_t per = std::max<int64_t>(1, ((1ll << 31) - 65536) / img);
+  for (int64_t n0 = 0; n0 < a_in.N; n0 += per) {
+    L1BlockArgs a = a_in;
+    a.N = (int)std::min<int64_t>(per, a_in.N - n0);
+    a.x = a_in.x + n0 * img / 2;
+    a.out = a_in.out + n0 * img / 2;
+    a.x_bytes = a.N * img;
+    const int64_t tiles = (int64_t)a.N * (a.H / 16) * (a.W / 16);
+    const int64_t g = std::min<int64_t>(tiles, 256);
+    hipLaunchKernelGGL(l1block_kernel, dim3((unsigned)g), dim3(256), SMEM, s, a);
+    SAD_CHECK_HIP(hipGetLastError());
+  }
+  return SAD_OK;
+}
+
+}  // namespace sad

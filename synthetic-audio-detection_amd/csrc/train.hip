@@ -891,7 +891,7 @@ extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_
   a.Cout = Cout;
   a.M = N * a.Ho * a.Wo;
   const int64_t P = a.M;
-  const int v = default_block_variant(a, dtype);
+  int v = default_block_variant(a, dtype);
   // The fused statistics need ONE launch (one partial row per workgroup).  A
   // batch whose operands pass the kernels' 32-bit buffer range (e.g. a
   // Bottleneck's 256-channel 128^2 layer1 maps at ~256 images) is split by
@@ -899,6 +899,9 @@ extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_
   // plain conv launches, then bn_reduce over the stored output.
   const int64_t es = dtype == SAD_F32 ? 4 : 2, lim = (1ll << 31) - 65536;
   const bool one_launch = N * H * W * Cin * es < lim && a.M * Cout * es < lim;
+  // the patch-resident layer3/4 kernels (30, 31) sum no statistics; their
+  // implicit-GEMM counterpart (13) does
+  if ((v == 30 || v == 31) && dtype == SAD_BF16 && one_launch) v = 13;
   const bool fused = dtype == SAD_BF16 && one_launch && (v == 13 || v == 15 || v == 20 || v == 25);
   int rows = 0;
   if (fused) {

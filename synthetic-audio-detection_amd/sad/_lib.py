@@ -91,6 +91,7 @@ SIGNATURES = {
     'sad_conv2d_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P]),
     'sad_block_conv_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, I32, I32, I32, I32, P, I32, P, P, P, I32, I32,
                                           I32, I32, I32, I32, I32, P]),
+    'sad_l1_block_run': (ctypes.c_int, [P, I64, I32, I32, P, I32, P, P, I32, P, P, I32, P]),
     'sad_synth_pcm': (ctypes.c_int, [ctypes.c_uint64, I64, I64, I32, P, P]),
     # training (include/sad.h "training")
     'sad_specaug_norm_run': (ctypes.c_int, [P, I64, I32, I32, P, P, P]),

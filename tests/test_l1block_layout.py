@@ -1,0 +1,138 @@
+"""CPU: the fused layer1 BasicBlock kernel's LDS layouts (csrc/l1block.hip,
+variant 40), checked exhaustively with the kernel's own index formulas.
+
+* conv1's 21 fragments per tile (18 row-aligned + 3 leftover column-16/17
+  fragments, split over the two pixel-group waves) cover every pixel of the
+  18 x 18 intermediate, and every lane that does not own a live pixel
+  duplicates one that does (its writes are then identical);
+* every ds_read_b128 fragment read (conv1 from the 20 x 20 input patch, conv2
+  from the intermediate) is free of LDS bank conflicts under the MI355X
+  ds_read_b128 lane grouping (MI355X_MICROARCH.md, LDS table: 4 groups of 16
+  lanes, bank = (byte address / 4) mod 64);
+* the DMA's source-side swizzle and the readers' swizzle agree (each lane reads
+  the chunk it asked for).
+"""
+KEY = 0xd92dad912240
+GROUPS = [[0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27],
+          [4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31]]
+GROUPS += [[l + 32 for l in g] for g in GROUPS]
+PWD, IWD, PROW, IROW = 20, 18, 20 * 128, 18 * 128
+
+
+def key(x):
+    return (KEY >> (3 * x)) & 7
+
+
+def patch_pos(Y, X, c):
+    """position of chunk c in patch row (Y, X)"""
+    return c ^ key(X) ^ ((Y & 3) << 1)
+
+
+def lds_cycles(addrs):
+    tot = 0
+    for g in GROUPS:
+        banks = {}
+        for l in g:
+            a = addrs[l]
+            for d in range(4):
+                banks.setdefault((a // 4 + d) % 64, set()).add(a)
+        tot += max(len(v) for v in banks.values())
+    return tot
+
+
+def conv1_fragment(pg, k, ln):
+    """intermediate pixel (y, x) of lane ln in conv1 fragment k of pixel group pg"""
+    fr = ln & 15
+    if k < 9:
+        return 9 * pg + k, fr
+    m = pg if k == 9 else 2 + pg
+    return min(8 * m + (fr >> 1), IWD - 1), 16 + (fr & 1)
+
+
+def conv1_addr(pg, k, ln, ky, kx, h):
+    """the kernel's rd1 address (patch buffer 0)"""
+    fr, fg = ln & 15, ln >> 4
+    if k < 9:
+        Y = 9 * pg + k + ky
+        LA = (fr + kx) * 128 + ((fg ^ key(fr + kx)) << 4)
+        sg = ((Y & 3) << 5) ^ (h << 6)
+        return (LA ^ sg) + pg * 9 * PROW + (k + ky) * PROW
+    l = k - 9
+    m = pg if l == 0 else 2 + pg
+    e = fr & 1
+    LY = min(8 * m + (fr >> 1), IWD - 1)
+    LR0 = (LY * PWD + 16 + e) * 128
+    KX = fg ^ key(16 + e + kx)
+    pos = KX ^ (((LY + ky) & 3) << 1) ^ (h << 2)
+    return LR0 + (pos << 4) + (ky * PWD + kx) * 128
+
+
+def test_conv1_fragments_cover_the_intermediate():
+    live = set()
+    for pg in range(2):
+        for k in range(11):
+            for ln in range(16):
+                live.add(conv1_fragment(pg, k, ln))
+    assert live == {(y, x) for y in range(IWD) for x in range(IWD)}
+
+
+def test_conv1_reads_are_conflict_free_and_hit_the_right_chunk():
+    for pg in range(2):
+        for k in range(11):
+            for ky in range(3):
+                for kx in range(3):
+                    for h in range(2):
+                        addrs = [conv1_addr(pg, k, ln, ky, kx, h) for ln in range(64)]
+                        for ln in range(64):
+                            y, x = conv1_fragment(pg, k, ln)
+                            Y, X, c = y + ky, x + kx, (ln >> 4) + 4 * h
+                            assert addrs[ln] == (Y * PWD + X) * 128 + (patch_pos(Y, X, c) << 4)
+                        # the partial leftover fragments (m = 2, 3) duplicate lanes: broadcast
+                        assert lds_cycles(addrs) == 4, (pg, k, ky, kx, h)
+
+
+def test_conv2_reads_are_conflict_free():
+    for pg in range(2):
+        for jj in range(8):
+            for ky in range(3):
+                for kx in range(3):
+                    for h in range(2):
+                        addrs = []
+                        for ln in range(64):
+                            fr, fg = ln & 15, ln >> 4
+                            I2 = pg * 8 * IROW + (((fr + kx) * 128 + ((fg ^ key(fr + kx)) << 4)) ^ (h << 6))
+                            a = I2 + (jj + ky) * IROW
+                            p, c = (8 * pg + jj + ky) * IWD + fr + kx, fg + 4 * h
+                            assert a == p * 128 + ((c ^ key(fr + kx)) << 4)
+                            addrs.append(a)
+                        assert lds_cycles(addrs) == 4
+
+
+def test_residual_address_is_the_patch_centre():
+    for pg in range(2):
+        for jj in range(8):
+            for cg in range(2):
+                for i in range(2):
+                    for ln in range(64):
+                        fr, fg = ln & 15, ln >> 4
+                        cw = 32 * cg
+                        LRr = (fr + 2) * 128 + ((((cw >> 3) + 2 * i + (fg >> 1)) ^ key(fr + 2)) << 4) + (fg & 1) * 8
+                        a = (LRr ^ (((jj + 2) & 3) << 5)) + pg * 8 * PROW + (jj + 2) * PROW
+                        Y, X = 8 * pg + jj + 2, fr + 2
+                        co = cw + 16 * i + 4 * fg
+                        assert a == (Y * PWD + X) * 128 + (patch_pos(Y, X, co >> 3) << 4) + (co & 7) * 2
+
+
+def test_dma_swizzle_matches_the_readers():
+    # piece q, lane ln writes LDS position ln & 7 of patch row 8q + ln/8 with
+    # source chunk (ln & 7) ^ key(X) ^ 2 (Y & 3): that must be the chunk the
+    # readers expect at that position
+    for q in range(50):
+        for ln in range(64):
+            r = 8 * q + (ln >> 3)
+            Y = (r * 205) >> 12
+            assert Y == r // 20
+            X = r - 20 * Y
+            pos = ln & 7
+            c = pos ^ key(X) ^ ((Y & 3) << 1)
+            assert patch_pos(Y, X, c) == pos
