@@ -328,12 +328,13 @@ static int timed_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, do
   return rc;
 }
 
-// SAD_L1_FUSED=1 runs layer1's blocks on the fused BasicBlock kernel (variant
-// 40) instead of two convs per block (variant 25; A/B switch, off until faster)
+// SAD_L1_FUSED=0 runs layer1's blocks as two convs each (variant 25) instead of
+// the fused BasicBlock kernel (variant 40; A/B switch).  Same box, 2 rounds:
+// fused with 128-segment front sub-batches 52.5k seg/s vs 51.5k unfused at 32
 static bool l1_fused() {
   static const bool v = [] {
     const char* e = getenv("SAD_L1_FUSED");
-    return e ? atoi(e) != 0 : false;
+    return e ? atoi(e) != 0 : true;
   }();
   return v;
 }
@@ -502,12 +503,17 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
 // slower (layer2's grids underfill).  At 32:128 one box measured -1.1%.
 // Round 2 at micro-batch 1024: 40 is 0.9 % and 48 1.4 % slower than 32 (same
 // box, 3 rounds; profiles/r02s3_frontmb_ab.log).
-static int front_sub_batch() {
+// With layer1 fused (bf16, variant 40) only the block inputs/outputs pass
+// through memory and the fused kernel's per-workgroup weight prologue wants
+// more tiles: 128 segments (+1.8-2.1 % end to end vs fused at 32, same box;
+// 64: +1.7-2 %).
+static int front_sub_batch(int dtype) {
   static int v = [] {
     const char* e = getenv("SAD_FRONT_MB");
-    return e ? atoi(e) : 32;
+    return e ? atoi(e) : -1;
   }();
-  return v;
+  if (v >= 0) return v;
+  return dtype == SAD_BF16 && l1_fused() ? 128 : 32;
 }
 
 static int run_chunk(const sad_backbone_plan* p, const float* map, const float* img, int64_t mb, float* feats,
@@ -522,7 +528,7 @@ static int run_chunk(const sad_backbone_plan* p, const float* map, const float* 
   bool pooled = false;  // the last conv wrote the pooled features itself
   if (p->block_path) {
     const size_t es = p->dtype == SAD_BF16 ? 2 : 4;
-    const int64_t f = front_sub_batch() > 0 ? std::min<int64_t>(front_sub_batch(), mb) : mb;
+    const int64_t f = front_sub_batch(p->dtype) > 0 ? std::min<int64_t>(front_sub_batch(p->dtype), mb) : mb;
     // stem + layer1 per sub-chunk of f segments (Infinity-Cache-sized); layer1's
     // output ([f, 128, 128, 64] per sub-chunk) is gathered in bufD, then layers
     // 2-4 run on the whole micro-batch (layer2's halo grids underfill at f = 32:

@@ -785,15 +785,20 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
   if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo())))
     return a.Cout == 128 && !a.res && halo_c128_variant() == 22 ? 22 : 20;
-  // small maps (the trainer's 64-segment layer4: M = 16384): 256x256 tiles would
-  // leave CUs idle (one workgroup per CU), so split the channel tile (variant
-  // 15, 128x256).  Both keep the 256-pixel tile and the same K order, so the
-  // results (incl. the fused average pool) do not depend on the choice.
-  // layer3/4 stride-1 convs (persistent, one 256-channel x 16 x 16 tile per
-  // workgroup: only when the tiles cover the CUs, else variant 15 below)
-  // (bf16 only: the fp32 parity path stays on the implicit GEMM)
-  if (dtype == SAD_BF16 && halo256_mode() != 0 && halo256_ok(a) && a.M / 256 * (a.Cout / 256) >= block_device_cus())
-    return halo256_mode() == 2 ? 31 : 30;
+  // layer3/4 stride-1 convs: the patch-resident kernels (bf16 only: the fp32
+  // parity path stays on the implicit GEMM), chosen whatever the grid size: variants 30/31 sum K in a different order than
+  // 13/15, and a batch-size-dependent switch would make results depend on the
+  // micro-batch (a 1-rank and a 2-rank run of the same segments must agree
+  // bit for bit)
+  if (dtype == SAD_BF16 && halo256_mode() != 0 && halo256_ok(a)) return halo256_mode() == 2 ? 31 : 30;
+  return gemm_block_variant(a);
+}
+// the implicit-GEMM choice (also the fused-statistics path's: 30/31 sum no
+// statistics).  Small maps (the trainer's 64-segment layer4: M = 16384): 256x256
+// tiles would leave CUs idle (one workgroup per CU), so split the channel tile
+// (variant 15, 128x256).  Both keep the 256-pixel tile and the same K order, so
+// the results (incl. the fused average pool) do not depend on the choice.
+int gemm_block_variant(const BlockConvArgs& a) {
   if (a.Cout % 256 == 0)
     return a.res || (a.M + 255) / 256 * (a.Cout / 256) >= block_device_cus() ? 13 : 15;  // 13: residual epilogue
   return a.Cout % 128 == 0 ? c128_variant() : 9;

@@ -91,6 +91,7 @@ struct L1BlockArgs {
   const float* b2;
   int64_t x_bytes;       // set by launch_l1block
   int ablate;            // timing ablations (wrong results): 1 no patch DMA in the loop, 8 no epilogues
+  uint64_t* stamps;      // diagnostic builds only (-DSAD_STAMPS): s_memtime per tile phase
 };
 int launch_l1block(const L1BlockArgs& a, hipStream_t s);
 
@@ -119,6 +120,7 @@ int launch_stem_train(const StemArgs& a, hipStream_t s);
 constexpr int STEM_TRAIN_PARTS = 16;  // statistic partials per image (128 pooled rows / STEM_P)
 int launch_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, int variant = 0);
 int default_block_variant(const BlockConvArgs& a, int dtype);
+int gemm_block_variant(const BlockConvArgs& a);  // default_block_variant without 30/31 (bf16)
 bool layer2_halo();
 bool block_conv_can_pool(const BlockConvArgs& a, int dtype);  // default variant pools Ho x Wo tiles  // SAD_L2_HALO (default 1): layer2's identity blocks on the halo kernel
 // dx (+)= col2im(dcol) (train.hip; the strided dgrad of wgrad.hip)

@@ -45,7 +45,14 @@
 #include "igemm.hpp"
 #include "kernels.hpp"
 
+#include <stdio.h>
+
 #include <utility>
+#include <vector>
+
+#ifndef SAD_STAMPS
+#define SAD_STAMPS 0
+#endif
 
 namespace sad {
 
@@ -65,12 +72,17 @@ constexpr int NF = NA + 2;                 // + 2 leftover fragments
 constexpr int NS = 18;                     // K-steps per conv: 9 taps x 2 halves of 32 channels
 constexpr int NU1 = NS * NF;               // conv1 (read, 2 MFMA) units per wave
 constexpr int NU2 = NS * 8;                // conv2 units per wave
-constexpr int DQ = 4;                      // fragment reads in flight ahead of their MFMAs
+constexpr int DQ = 6;                      // fragment reads in flight ahead of their MFMAs
+constexpr int SA = 6;                      // conv1 K-steps run K-step-outer (the rest fragment-outer)
+constexpr int NB1 = NS - SA;
 constexpr int W2V = 8;                     // conv2 K-steps of channel tile 1 whose weights sit in VGPRs
 constexpr int BAD = 0x7FFFFFF0;
 constexpr uint64_t KEY = 0xd92dad912240ull;  // variant 30's column key (columns 18, 19: 0)
 static_assert(SMEM <= 160 * 1024, "LDS budget");
 static_assert(NDP % 2 == 0, "pieces");
+// conv1 unit u -> (K-step, fragment): phase A K-step-outer, phase B fragment-outer
+constexpr int l1b_s1(int u) { return u < SA * NF ? u / NF : SA + (u - SA * NF) % NB1; }
+constexpr int l1b_k1(int u) { return u < SA * NF ? u % NF : (u - SA * NF) / NB1; }
 }  // namespace l1b
 
 __device__ __forceinline__ int l1b_key(int x) { return (int)((l1b::KEY >> (3 * x)) & 7); }
@@ -87,6 +99,12 @@ __device__ __forceinline__ void l1b_mfma_a0(f32x4& acc, const l1b_v4& w, const u
 __device__ __forceinline__ void l1b_mfma_a(f32x4& acc, const l1b_v4& w, const uint4& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(__builtin_bit_cast(l1b_v4, b)));
 }
+// acc = c + w . b (the first K-step: C = the bias)
+__device__ __forceinline__ void l1b_mfma_ac(f32x4& acc, const l1b_v4& w, const uint4& b, const f32x4& c) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %3"
+               : "=&v"(acc)
+               : "a"(w), "v"(__builtin_bit_cast(l1b_v4, b)), "v"(c));
+}
 // the same with the weights in VGPRs (the AGPR file holds 256 of the 288)
 __device__ __forceinline__ void l1b_mfma_v0(f32x4& acc, const l1b_v4& w, const uint4& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(w), "v"(__builtin_bit_cast(l1b_v4, b)));
@@ -97,6 +115,12 @@ __device__ __forceinline__ void l1b_mfma_v(f32x4& acc, const l1b_v4& w, const ui
 // two floats -> packed bf16 pair (RNE), one v_cvt_pk_bf16_f32
 typedef __bf16 l1b_bf2 __attribute__((ext_vector_type(2)));
 typedef float l1b_f2 __attribute__((ext_vector_type(2)));
+// relu of an asm MFMA result (fmaxf would first canonicalise it: one more VALU)
+__device__ __forceinline__ float l1b_relu(float x) {
+  float r;
+  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 __device__ __forceinline__ uint32_t l1b_pk(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((l1b_f2){lo, hi}, l1b_bf2));
 }
@@ -129,12 +153,11 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
   const __amdgpu_buffer_rsrc_t ro =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)a.x_bytes, 0x00020000);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  const int ab = a.ablate;  // timing ablations (wrong results): 1 no patch DMA in the loop, 8 no epilogues
+  const int ab = a.ablate;  // timing ablation (wrong results): 1 no patch DMA in the loop
 
   // ---- patch piece k of this wave (q = wave + 4k: rows 8q .. 8q+7): the
   // lane's patch pixel (Y, X) and its source offset from the tile origin are
-  // tile-independent (computed once); a tile away from the image border needs
-  // no bounds test
+  // tile-independent (computed once)
   int DREL[QP], DYX[QP];
 #pragma unroll
   for (int k = 0; k < QP; ++k) {
@@ -147,7 +170,6 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
   // tile t's origin: image byte offset, (oy0, ox0), interior flag (uniform)
   struct TileO {
     int base, oy0, ox0;
-    bool inner;
   };
   auto tile_o = [&](int t) __attribute__((always_inline)) {
     const int b = t / tiles_img, rem = t - b * tiles_img;
@@ -156,17 +178,15 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
     o.oy0 = ty * 16;
     o.ox0 = (rem - ty * tiles_x) * 16;
     o.base = ((b * a.H + o.oy0) * a.W + o.ox0) * 128;
-    o.inner = o.oy0 >= 2 && o.oy0 + 18 <= a.H && o.ox0 >= 2 && o.ox0 + 18 <= a.W;
     return o;
   };
+  // (branch-free: the bounds test is VALU in the MFMA shadow; only the piece
+  // count per wave is a uniform branch)
   auto issue_piece = [&](int k, const TileO& o, int buf) __attribute__((always_inline)) {
     if (wave + NW * k >= NDP) return;  // uniform
-    int off = o.base + DREL[k];
-    if (!o.inner) {
-      const int Y = DYX[k] & 0xFFFF, X = DYX[k] >> 16;
-      if (!((unsigned)(o.oy0 - 2 + Y) < (unsigned)a.H && (unsigned)(o.ox0 - 2 + X) < (unsigned)a.W)) off = BAD;
-    }
-    dma16_m0(rx, off, lds0 + buf * PATCH + (wave + NW * k) * 1024);
+    const int Y = DYX[k] & 0xFFFF, X = DYX[k] >> 16;
+    const bool ok = (unsigned)(o.oy0 - 2 + Y) < (unsigned)a.H && (unsigned)(o.ox0 - 2 + X) < (unsigned)a.W;
+    dma16_m0(rx, ok ? o.base + DREL[k] : BAD, lds0 + buf * PATCH + (wave + NW * k) * 1024);
   };
 
   // ---- weights of both convs into registers: lane (fr, fg) of K-step s =
@@ -194,10 +214,27 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
   asm volatile("" ::: "memory");
 
 
+  // diagnostic build (-DSAD_STAMPS=1): s_memtime of waves 0 and 2 of
+  // workgroup 0 per tile -- 0 tile start, 1 conv1 issued, 2 after the
+  // intermediate barrier, 3 conv2 issued, 4 after the tile barrier
+  const bool stamp_on = SAD_STAMPS && a.stamps && blockIdx.x == 0 && (wave == 0 || wave == 2);
+  auto stamp = [&](int g, int slot) __attribute__((always_inline)) {
+    if constexpr (SAD_STAMPS) {
+      if (stamp_on && g < 1024) {
+        __builtin_amdgcn_sched_barrier(0);
+        uint64_t t_;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (lane == 0) a.stamps[(size_t)(wave >> 1) * 8192 + (size_t)g * 8 + slot] = t_;
+      }
+    }
+  };
   int pb = 0;
   for (int t = tp_begin; t < tp_end; ++t) {
+    stamp(t - tp_begin, 0);
     const bool has_next = t + 1 < tp_end;
     const TileO onext = tile_o(has_next ? t + 1 : t);
+    const bool dma_on = has_next && !(ab & 1);
     const int b = t / tiles_img, rem = t - b * tiles_img;
     const int ty = rem / tiles_x;
     const int oy0 = ty * 16, ox0 = (rem - ty * tiles_x) * 16;
@@ -225,9 +262,17 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
     }
 
     // ---------------- conv1: 18 x 18 intermediate ----------------
+    // Unit = one fragment read + its two MFMAs (channel tiles i = 0, 1).
+    // Phase A (K-steps s < SA) runs K-step-outer over the 11 fragments and
+    // carries the next tile's patch DMA; phase B runs fragment-outer over the
+    // remaining K-steps, so fragments complete one by one and fragment k-1's
+    // epilogue (ReLU, bf16, 0 outside the image, intermediate store) is issued
+    // among fragment k's MFMAs instead of after all of them (one wave per
+    // SIMD: VALU work only hides in the MFMA shadow).  The bias is the first
+    // MFMA's C operand.
     auto rd1 = [&](auto uc) __attribute__((always_inline)) -> uint4 {
       constexpr int u = decltype(uc)::value;
-      constexpr int s = u / NF, k = u % NF;
+      constexpr int s = l1b_s1(u), k = l1b_k1(u);
       constexpr int tap = s >> 1, h = s & 1, ky = tap / 3, kx = tap % 3;
       if constexpr (k < NA) {
         const int Y = 9 * pg + k + ky;                       // uniform
@@ -239,68 +284,108 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
         return *(const uint4*)(smem + (LR0t[l] + pbo + (pos << 4)) + (ky * PWD + kx) * 128);
       }
     };
+    f32x4 b1v[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) b1v[i] = *(const f32x4*)(smem + OFF_B + (cw + 16 * i + fgt * 4) * 4);
+    // column masks of this tile's intermediate pixels (0: outside the image):
+    // aligned fragments x = frt, leftovers x = 16 + et
+    const uint32_t cma = (unsigned)(ox0 - 1 + frt) < (unsigned)a.W ? 0xFFFFFFFFu : 0u;
+    const uint32_t cml = (unsigned)(ox0 + 15 + et) < (unsigned)a.W ? 0xFFFFFFFFu : 0u;
     f32x4 acc[2][NF];
+    // epilogue of fragment k in 4 parts (channel tile i = part / 2; first or
+    // second half of the 4 values), so it can be spread between MFMAs
+    uint32_t e1_inm = 0, e1_qx = 0;
+    int e1_addr = 0;
+    auto epi1 = [&](auto kc, auto pc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value, part = decltype(pc)::value, i = part >> 1;
+      if constexpr (part == 0) {
+        int y, x;
+        if constexpr (k < NA) {
+          y = 9 * pg + k;
+          x = frt;
+          e1_inm = (unsigned)(oy0 - 1 + y) < (unsigned)a.H ? cma : 0u;  // row test uniform
+        } else {
+          y = LYt[k - NA];
+          x = 16 + et;
+          e1_inm = (unsigned)(oy0 - 1 + y) < (unsigned)a.H ? cml : 0u;
+        }
+        e1_addr = OFF_I + (y * IWD + x) * 128 + (((cw >> 3) + (fgt >> 1)) ^ l1b_key(x)) * 16 + (fgt & 1) * 8;
+      }
+      if constexpr ((part & 1) == 0) {
+        e1_qx = l1b_pk(l1b_relu(acc[i][k][0]), l1b_relu(acc[i][k][1])) & e1_inm;
+      } else {
+        uint2 q;
+        q.x = e1_qx;
+        q.y = l1b_pk(l1b_relu(acc[i][k][2]), l1b_relu(acc[i][k][3])) & e1_inm;
+        // channel tile 1 is chunk + 2: position (c + 2) ^ key = (c ^ key) ^ 2 (c even)
+        *(uint2*)(smem + (i ? (e1_addr ^ 32) : e1_addr)) = q;
+      }
+    };
     uint4 bq[DQ];
     l1b_for<DQ>([&](auto uc) __attribute__((always_inline)) { bq[decltype(uc)::value] = rd1(uc); });
     l1b_for<NU1>([&](auto uc) __attribute__((always_inline)) {
       constexpr int u = decltype(uc)::value;
-      constexpr int s = u / NF, k = u % NF;
+      constexpr int s = l1b_s1(u), k = l1b_k1(u);
       const uint4 bf = bq[u % DQ];
       if constexpr (u + DQ < NU1) bq[u % DQ] = rd1(std::integral_constant<int, u + DQ>{});
-      if constexpr (k == 0 && s < QP)
-        if (has_next && !(ab & 1)) issue_piece(s, onext, pb ^ 1);
+      if constexpr (u % 5 == 0 && u / 5 < QP)
+        if (dma_on) issue_piece(u / 5, onext, pb ^ 1);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         if constexpr (s == 0)
-          l1b_mfma_a0(acc[i][k], w1r[i][s], bf);
+          l1b_mfma_ac(acc[i][k], w1r[i][s], bf, b1v[i]);
         else
           l1b_mfma_a(acc[i][k], w1r[i][s], bf);
       }
+      // fragment k-1 is complete: its epilogue parts go after units 2, 4, 6, 8
+      // of fragment k (>= 6 MFMAs after its last one: the XDL -> VALU read
+      // distance; the asm MFMAs keep compiler code from moving across them)
+      if constexpr (u >= SA * NF && k >= 1) {
+        constexpr int q = (u - SA * NF) % NB1;
+        if constexpr (q >= 2 && q <= 8 && q % 2 == 0)
+          epi1(std::integral_constant<int, k - 1>{}, std::integral_constant<int, q / 2 - 1>{});
+      }
     });
-    // the asm MFMAs' results are read by compiler code next: 8-pass XDL write
-    // -> VALU read needs 12 wait states, which hipcc does not pad for asm
+    stamp(t - tp_begin, 1);
+    // the last fragment: asm MFMA results read by compiler code need 12 wait
+    // states (8-pass XDL), which hipcc does not pad for asm
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 11" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    l1b_for<4>([&](auto pc) __attribute__((always_inline)) { epi1(std::integral_constant<int, NF - 1>{}, pc); });
 
-    // ---- conv1 epilogue: relu(acc + b1) (0 outside the image) -> intermediate
-    if (!(ab & 8)) {
+    // conv2's accumulators start at b2 + x (the identity): residual of output
+    // row 8pg + jj, channels cw + 16 i + 4 fg2, from the patch centre
+    int ln2;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln2) : "v"(lane));
+    const int fr2 = ln2 & 15, fg2 = ln2 >> 4;
+    int LRr[2];
 #pragma unroll
-      for (int k = 0; k < NF; ++k) {
-        int y, x;
-        if (k < NA) {
-          y = 9 * pg + k;
-          x = frt;
-        } else {
-          y = LYt[k - NA];
-          x = 16 + et;
-        }
-        const bool in = (unsigned)(oy0 - 1 + y) < (unsigned)a.H && (unsigned)(ox0 - 1 + x) < (unsigned)a.W;
-        const uint32_t inm = in ? 0xFFFFFFFFu : 0u;  // (0 outside the image: conv2's zero padding)
-        const int p = y * IWD + x;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const float4 b4 = *(const float4*)(smem + OFF_B + (cw + 16 * i + fgt * 4) * 4);
-          const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[i][k][r] + bb[r], 0.f);
-          uint2 q;
-          q.x = l1b_pk(v[0], v[1]) & inm;
-          q.y = l1b_pk(v[2], v[3]) & inm;
-          const int c = (cw >> 3) + 2 * i + (fgt >> 1);
-          *(uint2*)(smem + OFF_I + p * 128 + ((c ^ l1b_key(x)) << 4) + (fgt & 1) * 8) = q;
-        }
+    for (int i = 0; i < 2; ++i)
+      LRr[i] = (fr2 + 2) * 128 + ((((cw >> 3) + 2 * i + (fg2 >> 1)) ^ l1b_key(fr2 + 2)) << 4) + (fg2 & 1) * 8;
+    f32x4 acc2[2][8];
+    auto init2 = [&](auto jc, auto ic) __attribute__((always_inline)) {
+      constexpr int jj = decltype(jc)::value, i = decltype(ic)::value;
+      {
+        const f32x4 b4 = *(const f32x4*)(smem + OFF_B + 256 + (cw + 16 * i + fg2 * 4) * 4);
+        const uint2 rv = *(const uint2*)(smem + ((LRr[i] ^ (((jj + 2) & 3) << 5)) + pbo + pg * 8 * PROW) +
+                                         (jj + 2) * PROW);
+        acc2[i][jj][0] = b4[0] + __uint_as_float(rv.x << 16);
+        acc2[i][jj][1] = b4[1] + __uint_as_float(rv.x & 0xFFFF0000u);
+        acc2[i][jj][2] = b4[2] + __uint_as_float(rv.y << 16);
+        acc2[i][jj][3] = b4[3] + __uint_as_float(rv.y & 0xFFFF0000u);
       }
-    }
+    };
+    init2(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    init2(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 
+    stamp(t - tp_begin, 2);
     // ---------------- conv2 + identity ----------------
-    int ln2;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(ln2) : "v"(lane));
-    const int fr2 = ln2 & 15, fg2 = ln2 >> 4;
+    // Fragment-outer throughout: fragment jj-1's epilogue (ReLU, bf16, 8-B
+    // stores) and fragment jj+1's accumulator init go among fragment jj's MFMAs.
     // conv2: intermediate fragments of output rows 8pg + jj
     int I2[3][2];
 #pragma unroll
@@ -310,68 +395,59 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
         I2[kx][h] = OFF_I + pg * 8 * IROW + (((fr2 + kx) * 128 + ((fg2 ^ l1b_key(fr2 + kx)) << 4)) ^ (h << 6));
     auto rd2 = [&](auto uc) __attribute__((always_inline)) -> uint4 {
       constexpr int u = decltype(uc)::value;
-      constexpr int s = u / 8, jj = u % 8;
+      constexpr int s = u % NS, jj = u / NS;
       constexpr int tap = s >> 1, h = s & 1, ky = tap / 3, kx = tap % 3;
       return *(const uint4*)(smem + I2[kx][h] + (jj + ky) * IROW);
     };
-    f32x4 acc2[2][8];
+    const int obase = ((b * a.H + oy0 + 8 * pg) * a.W + ox0) * 128;  // uniform
+    // epilogue of fragment jj in 4 parts, as conv1's
+    uint32_t e2_qx = 0;
+    auto epi2 = [&](auto jc, auto pc) __attribute__((always_inline)) {
+      constexpr int jj = decltype(jc)::value, part = decltype(pc)::value, i = part >> 1;
+      if constexpr ((part & 1) == 0) {
+        e2_qx = l1b_pk(l1b_relu(acc2[i][jj][0]), l1b_relu(acc2[i][jj][1]));
+      } else {
+        uint2 q;
+        q.x = e2_qx;
+        q.y = l1b_pk(l1b_relu(acc2[i][jj][2]), l1b_relu(acc2[i][jj][3]));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(l1b_v2, q), ro,
+                                              (jj * a.W + fr2) * 128 + (cw + 16 * i + 4 * fg2) * 2, obase, 0);
+      }
+    };
     l1b_for<DQ>([&](auto uc) __attribute__((always_inline)) { bq[decltype(uc)::value] = rd2(uc); });
     l1b_for<NU2>([&](auto uc) __attribute__((always_inline)) {
       constexpr int u = decltype(uc)::value;
-      constexpr int s = u / 8, jj = u % 8;
+      constexpr int s = u % NS, jj = u / NS;
       const uint4 bf = bq[u % DQ];
       if constexpr (u + DQ < NU2) bq[u % DQ] = rd2(std::integral_constant<int, u + DQ>{});
       l1b_for<2>([&](auto ic) __attribute__((always_inline)) {
         constexpr int i = decltype(ic)::value;
         // the last K-steps' weights of channel tile 1 sit in VGPRs
-        constexpr bool wv = i == 1 && s >= NS - W2V;
-        if constexpr (s == 0)
-          l1b_mfma_a0(acc2[i][jj], w2r[i][s], bf);
-        else if constexpr (wv)
+        if constexpr (i == 1 && s >= NS - W2V)
           l1b_mfma_v(acc2[i][jj], w2r[i][s], bf);
         else
           l1b_mfma_a(acc2[i][jj], w2r[i][s], bf);
       });
+      // fragment jj-1's epilogue parts after units 2, 4, 6, 8 of fragment jj,
+      // fragment jj+1's accumulator init after units 10 and 12
+      if constexpr (jj >= 1 && s >= 2 && s <= 8 && s % 2 == 0)
+        epi2(std::integral_constant<int, jj - 1>{}, std::integral_constant<int, s / 2 - 1>{});
+      if constexpr (jj + 1 < 8 && (s == 10 || s == 12))
+        init2(std::integral_constant<int, jj + 1>{}, std::integral_constant<int, (s - 10) / 2>{});
     });
+    stamp(t - tp_begin, 3);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 11" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    l1b_for<4>([&](auto pc) __attribute__((always_inline)) { epi2(std::integral_constant<int, 7>{}, pc); });
 
-    // this wave's patch pieces of the next tile have landed (they went out
-    // during conv1); the stores below may stay in flight
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // ---- conv2 epilogue: relu(acc + b2 + x) -> out (8 B per lane)
-    if (!(ab & 8)) {
-      // residual (patch centre) of channels cw + 16 i + 4 fg2: pixel column fr2 + 2
-      int LRr[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        LRr[i] = (fr2 + 2) * 128 + ((((cw >> 3) + 2 * i + (fg2 >> 1)) ^ l1b_key(fr2 + 2)) << 4) + (fg2 & 1) * 8;
-      const int obase = ((b * a.H + oy0 + 8 * pg) * a.W + ox0) * 128;  // uniform
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const uint2 rv = *(const uint2*)(smem + ((LRr[i] ^ ((((jj + 2) & 3)) << 5)) + pbo + pg * 8 * PROW) +
-                                           (jj + 2) * PROW);
-          const float4 b4 = *(const float4*)(smem + OFF_B + 256 + (cw + 16 * i + fg2 * 4) * 4);
-          const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
-          float v[4];
-          v[0] = acc2[i][jj][0] + bb[0] + __uint_as_float(rv.x << 16);
-          v[1] = acc2[i][jj][1] + bb[1] + __uint_as_float(rv.x & 0xFFFF0000u);
-          v[2] = acc2[i][jj][2] + bb[2] + __uint_as_float(rv.y << 16);
-          v[3] = acc2[i][jj][3] + bb[3] + __uint_as_float(rv.y & 0xFFFF0000u);
-          uint2 q;
-          q.x = l1b_pk(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f));
-          q.y = l1b_pk(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(l1b_v2, q), ro, (jj * a.W + fr2) * 128 + (cw + 16 * i + 4 * fg2) * 2, obase, 0);
-        }
-      }
-    }
-    // the intermediate and patch pb are free, patch pb ^ 1 has landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // this wave's patch pieces of the next tile (issued in conv1) have landed
+    // -- the 16 output stores, younger, may stay in flight; then the
+    // intermediate and patch pb are free and patch pb ^ 1 is published
+    asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    stamp(t - tp_begin, 4);
     pb ^= 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -402,8 +478,37 @@ int launch_l1block(const L1BlockArgs& a_in, hipStream_t s) {
     a.x_bytes = a.N * img;
     const int64_t tiles = (int64_t)a.N * (a.H / 16) * (a.W / 16);
     const int64_t g = std::min<int64_t>(tiles, 256);
+#if SAD_STAMPS
+    static uint64_t* sbuf = nullptr;
+    if (!sbuf) SAD_CHECK_HIP(hipMalloc(&sbuf, 2 * 8192 * 8));
+    SAD_CHECK_HIP(hipMemsetAsync(sbuf, 0, 2 * 8192 * 8, s));
+    a.stamps = sbuf;
+#endif
     hipLaunchKernelGGL(l1block_kernel, dim3((unsigned)g), dim3(256), SMEM, s, a);
     SAD_CHECK_HIP(hipGetLastError());
+#if SAD_STAMPS
+    {  // per-tile phase averages of waves 0 and 2 of workgroup 0 (skipping the first tile)
+      std::vector<uint64_t> h(2 * 8192);
+      SAD_CHECK_HIP(hipStreamSynchronize(s));
+      SAD_CHECK_HIP(hipMemcpy(h.data(), sbuf, h.size() * 8, hipMemcpyDeviceToHost));
+      for (int wv = 0; wv < 2; ++wv) {
+        double ph[5] = {0, 0, 0, 0, 0};
+        int n = 0;
+        for (int t = 1; t + 1 < 1024; ++t) {
+          const uint64_t* c = &h[(size_t)wv * 8192 + (size_t)t * 8];
+          const uint64_t nxt = h[(size_t)wv * 8192 + (size_t)(t + 1) * 8];
+          if (!c[0] || !c[4] || !nxt) break;
+          for (int k = 0; k < 4; ++k) ph[k] += (double)(c[k + 1] - c[k]);
+          ph[4] += (double)(nxt - c[4]);
+          ++n;
+        }
+        if (n)
+          fprintf(stderr, "l1block stamps N=%d wave %d: %d tiles, cycles conv1 %.0f | epi1+B1 %.0f | conv2 %.0f | "
+                  "epi2+B2 %.0f | loop %.0f | total %.0f\n", a.N, 2 * wv, n, ph[0] / n, ph[1] / n, ph[2] / n,
+                  ph[3] / n, ph[4] / n, (ph[0] + ph[1] + ph[2] + ph[3] + ph[4]) / n);
+      }
+    }
+#endif
   }
   return SAD_OK;
 }

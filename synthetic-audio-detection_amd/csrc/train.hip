@@ -900,8 +900,8 @@ extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_
   const int64_t es = dtype == SAD_F32 ? 4 : 2, lim = (1ll << 31) - 65536;
   const bool one_launch = N * H * W * Cin * es < lim && a.M * Cout * es < lim;
   // the patch-resident layer3/4 kernels (30, 31) sum no statistics; their
-  // implicit-GEMM counterpart (13) does
-  if ((v == 30 || v == 31) && dtype == SAD_BF16 && one_launch) v = 13;
+  // implicit-GEMM counterparts (13 / 15) do
+  if ((v == 30 || v == 31) && dtype == SAD_BF16 && one_launch) v = gemm_block_variant(a);
   const bool fused = dtype == SAD_BF16 && one_launch && (v == 13 || v == 15 || v == 20 || v == 25);
   int rows = 0;
   if (fused) {

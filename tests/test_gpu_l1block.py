@@ -2,9 +2,11 @@
 variant 40) against
   (1) the unfused path it replaces -- conv1, then conv2 + identity on the
       resident-weight halo kernel (variant 25), through sad_block_conv_run:
-      both sum K in the same order (tap-major, two 32-channel halves per tap)
-      on the same MFMA and round the intermediate to bf16 once, so the outputs
-      must be BIT-identical;
+      both sum the taps in the same K order on the same MFMA, but the fused
+      kernel starts its accumulators at the bias (conv2: bias + identity)
+      where variant 25 adds them after the sum, so fp32 rounding differs and
+      an intermediate value can land one bf16 ulp apart; bar as (2), and at
+      most 1 % of the outputs may differ at all;
   (2) a torch fp32 reference of timm's BasicBlock with BN folded
       (inference_runner.py:49-51): mid = bf16(relu(conv(x, w1) + b1)),
       out = relu(conv(mid, w2) + b2 + x); bar: 1 bf16 ulp of |ref| + 1e-2.
@@ -64,14 +66,17 @@ def _torch_ref(x, w1, b1, w2, b2):
 
 
 @pytest.mark.parametrize('N,H,W', [(1, 16, 16), (2, 48, 32), (3, 128, 128), (5, 64, 80), (37, 128, 128)])
-def test_fused_block_bit_identical_to_unfused(N, H, W):
+def test_fused_block_matches_unfused(N, H, W):
     ops = _operands(N, H, W, N * 1000 + H + W)
     out = _fused(*ops)
     ref = _unfused(*ops)
     torch.cuda.synchronize()
     assert torch.isfinite(out.float()).all()
+    d = (out.float() - ref.float()).abs()
+    bound = ref.float().abs() * 2.0 ** -8 + 1e-2
+    assert bool((d <= bound).all()), f'max |d| {d.max().item():.3g}'
     nd = (out != ref).sum().item()
-    assert nd == 0, f'{nd} of {out.numel()} outputs differ; max |d| {(out.float() - ref.float()).abs().max().item()}'
+    assert nd <= out.numel() // 100, f'{nd} of {out.numel()} outputs differ'
 
 
 @pytest.mark.parametrize('N,H,W', [(1, 16, 16), (2, 48, 32), (32, 128, 128)])

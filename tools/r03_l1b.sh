@@ -1,0 +1,9 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_l1block.py > gpurun_out/r03_l1b_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r03_l1b_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/l1bench.py --n 32 256 --ablate 1 > gpurun_out/r03_l1b_bench.log 2>&1 || exit 1
+cat gpurun_out/r03_l1b_bench.log
+SAD_LIB=abl/libsad_l1stamps.so timeout -k 10 300 python -u tools/l1bench.py --n 256 > gpurun_out/r03_l1b_stamps.log 2>&1 || exit 1
+grep -m4 "stamps" gpurun_out/r03_l1b_stamps.log; grep "stamps" gpurun_out/r03_l1b_stamps.log | tail -4
+timeout -k 5 60 ./tools/mfma_ab_bin | tail -9
