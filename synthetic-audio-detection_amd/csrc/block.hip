@@ -714,6 +714,27 @@ static bool halo_ok(const BlockConvArgs& a, int dtype) {
 }
 // SAD_L2_HALO=0 runs layer2's second block on the implicit-GEMM kernel (identity
 // shortcut as MFMA columns) instead of the halo kernel (A/B switch)
+// SAD_L2_V31=1 runs layer2's stride-1 convs on variant 31 with 128-channel
+// tiles (4 channel groups x 2 pixel halves; identity / downsample as shortcut
+// columns) instead of the halo kernel (variant 20, identity as an epilogue
+// residual) and the implicit GEMM (variant 15, conv2 + downsample).  Measured
+// 2.2-2.7 % slower end to end (same box, 3 rounds: 52.4k vs 53.7k seg/s): at
+// 128 channels a K-step is half the MFMAs for the same per-step weight loads,
+// waits and chunk barriers.  Off by default; tested (test_gpu_blockconv.py).
+bool layer2_v31() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_L2_V31");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return v;
+}
+// variant 31's contract (either tile width): 3x3/s1/p1, 16 x 16 tiles, whole
+// 128-B chunks, no epilogue residual / statistics
+static bool halo31_ok(const BlockConvArgs& a) {
+  return a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Cout % 128 == 0 && a.H % 16 == 0 &&
+         a.W % 16 == 0 && a.Ho == a.H && a.Wo == a.W && !a.res && !a.st_part && a.Cin % 64 == 0 &&
+         (!a.in1 || a.Cin1 % 64 == 0) && (!a.pool_out || (a.H == 16 && a.W == 16 && a.Cout % 256 == 0));
+}
 bool layer2_halo() {
   static const bool v = [] {
     const char* e = getenv("SAD_L2_HALO");
@@ -783,6 +804,9 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
     return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   }
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
+  // layer2's 128-channel stride-1 convs (incl. conv2 + downsample / identity as
+  // shortcut columns): variant 31 with 128-channel tiles
+  if (dtype == SAD_BF16 && layer2_v31() && a.Cout == 128 && halo31_ok(a)) return 31;
   if (halo_ok(a, dtype) && (a.res || (a.Cout <= 128 && layer2_halo())))
     return a.Cout == 128 && !a.res && halo_c128_variant() == 22 ? 22 : 20;
   // layer3/4 stride-1 convs: the patch-resident kernels (bf16 only: the fp32
@@ -812,12 +836,14 @@ static int pool_tile(int v) {
   return 0;
 }
 bool block_conv_can_pool(const BlockConvArgs& a, int dtype) {
-  const int bp = pool_tile(default_block_variant(a, dtype));
-  return bp > 0 && a.Ho * a.Wo == bp && !a.res && a.M % bp == 0;
+  const int v = default_block_variant(a, dtype);
+  const int bp = pool_tile(v);
+  return bp > 0 && a.Ho * a.Wo == bp && !a.res && a.M % bp == 0 && (v != 31 || a.Cout % 256 == 0);
 }
 static bool variant_fits(int v, int cout) {
   if (v == 26) return cout == 64;
-  if (v == 30 || v == 31) return cout % 256 == 0;
+  if (v == 30) return cout % 256 == 0;
+  if (v == 31) return cout % 128 == 0;
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128, 128};
   if (v == 20 || v == 21) return cout % 64 == 0;
   if (v == 22) return cout % 128 == 0;
@@ -970,7 +996,7 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
 #endif
   }
   if (v == 31) {
-    SAD_REQUIRE(dtype == SAD_BF16 && halo256_ok(a_in), "variant 31: bf16 3x3/s1/p1, Cout % 256, 16 x 16 tiles");
+    SAD_REQUIRE(dtype == SAD_BF16 && halo31_ok(a_in), "variant 31: bf16 3x3/s1/p1, Cout % 128, 16 x 16 tiles");
     return launch_halo256r(a, s);
   }
   if (dtype == SAD_BF16X3 && v == 26) {

@@ -30,6 +30,11 @@
 // at the MFMA rate), 64 MFMA 16x16x32.  Accumulators 128 VGPRs (2 x 16 tiles).
 // Epilogue: register-only (bias, ReLU, bf16, 8-B stores) or the fused average
 // pool (a wave holds all 256 pixels of its channels: no cross-wave reduction).
+//
+// BC = 128 (layer2's 128-channel stride-1 convs): the 8 waves are 4 channel
+// groups x 2 pixel halves (rows 0-7 / 8-15 of the tile), so a wave keeps the
+// same 2 MFMAs per fragment read and the same weight-load count per K-step;
+// the two pixel halves of a channel group load the same weights (from L2).
 #include "common.hpp"
 #include "igemm.hpp"
 #include "kernels.hpp"
@@ -37,8 +42,7 @@
 namespace sad {
 
 namespace h31 {
-constexpr int NW = 8, TC = 2, TP = 16;  // waves; per wave 2 x 16 channels x 16 x 16 pixels
-constexpr int BC = 16 * TC * NW;        // 256 channels per workgroup
+constexpr int NW = 8, TC = 2;           // waves; per wave 2 x 16 channels
 constexpr int TW = 16, TH = 16, PW = TW + 2, PR = PW * (TH + 2);
 constexpr int NDP = (PR + 7) / 8;       // 41 pieces per conv chunk
 constexpr int SCR = PW * TH;            // shortcut chunk: slots ty * 18 + tx
@@ -46,7 +50,7 @@ constexpr int NDS = SCR / 8;            // 36 pieces per shortcut chunk
 constexpr int PATCH = NDP * 1024;
 constexpr int ROWB = PW * 128;
 constexpr int OFF_BIAS = 2 * PATCH;
-constexpr int SMEM = OFF_BIAS + BC * 4;
+constexpr int SMEM = OFF_BIAS + 256 * 4;
 constexpr int BAD = 0x7FFFFFF0;
 constexpr uint64_t KEY = 0xd92dad912240ull;  // variant 30's column key {0,0,1,1,2,2,4,4,5,5,6,6,2,2,6,6,0,0}
 static_assert(SMEM <= 160 * 1024, "LDS budget");
@@ -56,9 +60,13 @@ __device__ __forceinline__ int h31_key(int px) { return (int)((h31::KEY >> (3 * 
 
 typedef unsigned int h31_v4 __attribute__((ext_vector_type(4)));
 
-template <bool POOL>
+// BC channels per workgroup (256 or 128): NCG channel groups of 32 x NPG pixel
+// groups of TP tile rows
+template <int BC, bool POOL>
 __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   using namespace h31;
+  constexpr int NCG = BC / 32, NPG = NW / NCG, TP = 16 / NPG;
+  static_assert(NCG * NPG == NW && (!POOL || NPG == 1), "wave split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -72,7 +80,9 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   const int tp_begin = (int)((int64_t)wi * tiles_p / gp), tp_end = (int)((int64_t)(wi + 1) * tiles_p / gp);
   const int c0 = tc * BC;
   if (tp_begin >= tp_end) return;  // whole workgroup (uniform)
-  const int cw = c0 + wave * 16 * TC;  // this wave's first output channel
+  const int cgrp = wave % NCG, pgrp = wave / NCG;
+  const int cw = c0 + cgrp * 16 * TC;  // this wave's first output channel
+  const int r0w = pgrp * TP;           // this wave's first tile row
 
   const int cinb = a.Cin * 2;
   const int nc0 = cinb / 128;                    // conv chunks (9 taps each)
@@ -175,7 +185,7 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   // ---- one K-step: 64 MFMAs; the pixel fragment of output row j, half h is at
   // patch row j + ky, column kx + fr (shortcut chunks: ky = kx = 0)
   auto step = [&](int pbuf, int ky, int kx) __attribute__((always_inline)) {
-    const int pbase = pbuf * PATCH + ky * ROWB;
+    const int pbase = pbuf * PATCH + (ky + r0w) * ROWB;
     const int o0 = (kx + fr) * 128 + ((fg ^ h31_key(kx + fr)) << 4);
     const int o1 = (kx + fr) * 128 + (((fg + 4) ^ h31_key(kx + fr)) << 4);
     const char* pb0 = smem + pbase + o0;
@@ -229,7 +239,7 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
       u16* __restrict__ out = (u16*)a.out;
 #pragma unroll
       for (int j = 0; j < TP; ++j) {
-        const int64_t px = (int64_t)(b * a.H + oy0 + j) * a.W + ox0 + fr;
+        const int64_t px = (int64_t)(b * a.H + oy0 + r0w + j) * a.W + ox0 + fr;
 #pragma unroll
         for (int i = 0; i < TC; ++i) {
           const int co = cw + i * 16 + fg * 4;
@@ -299,19 +309,20 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool POOL>
+template <int BC, bool POOL>
 static int launch_halo256r_t(const BlockConvArgs& a, hipStream_t s) {
   using namespace h31;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)halo256r_kernel<POOL>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    (void)hipFuncSetAttribute((const void*)halo256r_kernel<BC, POOL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              SMEM);
     attr = true;
   }
   const int n_tc = a.Cout / BC;
   const int64_t tiles_p = (int64_t)a.N * (a.H / TH) * (a.W / TW);
   int64_t g = std::min<int64_t>(tiles_p * n_tc, 256);
   g = std::max<int64_t>(n_tc, g / n_tc * n_tc);
-  hipLaunchKernelGGL((halo256r_kernel<POOL>), dim3((unsigned)g), dim3(512), SMEM, s, a);
+  hipLaunchKernelGGL((halo256r_kernel<BC, POOL>), dim3((unsigned)g), dim3(512), SMEM, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }
@@ -320,7 +331,7 @@ static int launch_halo256r_t(const BlockConvArgs& a, hipStream_t s) {
 int launch_halo256r(const BlockConvArgs& a, hipStream_t s) {
   SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1, "variant 31: 3x3, stride 1, pad 1");
   SAD_REQUIRE(!a.res && !a.st_part, "variant 31: no epilogue residual / fused statistics (shortcut as in1)");
-  SAD_REQUIRE(a.Cout % h31::BC == 0, "variant 31: Cout must be a multiple of 256");
+  SAD_REQUIRE(a.Cout % 128 == 0, "variant 31: Cout must be a multiple of 128");
   SAD_REQUIRE(a.H % 16 == 0 && a.W % 16 == 0 && a.Ho == a.H && a.Wo == a.W, "variant 31: image must tile by 16 x 16");
   SAD_REQUIRE((a.Cin * 2) % 128 == 0 && (!a.in1 || (a.Cin1 * 2) % 128 == 0), "variant 31: whole 128-B chunks");
   SAD_REQUIRE(!a.in1 || ((a.Ho - 1) * a.ss1 < a.H1 && (a.Wo - 1) * a.ss1 < a.W1), "variant 31: shortcut source");
@@ -330,10 +341,11 @@ int launch_halo256r(const BlockConvArgs& a, hipStream_t s) {
   SAD_REQUIRE(a.out || a.pool_out, "null output");
   SAD_REQUIRE(a.M == (int64_t)a.N * a.H * a.W, "variant 31: M = N H W");
   if (a.pool_out) {
-    SAD_REQUIRE(a.H == 16 && a.W == 16, "variant 31 fused average pool: a 16 x 16 tile must be one image");
-    return launch_halo256r_t<true>(a, s);
+    SAD_REQUIRE(a.H == 16 && a.W == 16 && a.Cout % 256 == 0,
+                "variant 31 fused average pool: a 16 x 16 tile must be one image, Cout % 256");
+    return launch_halo256r_t<256, true>(a, s);
   }
-  return launch_halo256r_t<false>(a, s);
+  return a.Cout % 256 == 0 ? launch_halo256r_t<256, false>(a, s) : launch_halo256r_t<128, false>(a, s);
 }
 
 }  // namespace sad

@@ -72,6 +72,13 @@ CASES = [
     ('l4-ds-30', 3, 16, 256, 512, 1, 'ds', [30, 31]),
     ('l4-id-30', 5, 16, 512, 512, 1, 'id', [30, 31]),
     ('l4-plain-30-rect', 2, 32, 512, 512, 1, None, [30, 31]),
+    # variant 31 with 128-channel tiles (layer2: 4 channel groups x 2 pixel
+    # halves): plain, identity columns, the downsample from a 2x source (64 ch)
+    ('l2-plain-31', 3, 64, 128, 128, 1, None, [31]),
+    ('l2-plain-31-ragged', 9, 48, 128, 128, 1, None, [31]),
+    ('l2-id-31', 2, 64, 128, 128, 1, 'id', [31]),
+    ('l2-ds-31', 2, 32, 64, 128, 1, 'ds', [31]),
+    ('l3-two-tiles-31', 2, 16, 128, 384, 1, None, [31]),
 ]
 
 
