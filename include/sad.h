@@ -299,8 +299,7 @@ int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t W, int32_t
  * layer1 block -- reference inference_runner.py:49-51 (timm forward_features).
  * bf16 only.  x, out: NHWC [N,H,W,64] bf16 (must not overlap), H and W
  * multiples of 16; w1, w2: [64][w_ld] bf16, k = tap * 64 + ci; b1, b2: [64]
- * fp32.  ablate: 0 (timing-only bits otherwise, results wrong).  Async on
- * `stream`. */
+ * fp32.  ablate: reserved, pass 0.  Async on `stream`. */
 int sad_l1_block_run(const void* x, int64_t N, int32_t H, int32_t W, const void* w1, int32_t w1_ld,
                      const float* b1, const void* w2, int32_t w2_ld, const float* b2, void* out,
                      int32_t ablate, void* stream);

@@ -49,8 +49,7 @@ constexpr int SCR = PW * TH;            // shortcut chunk: slots ty * 18 + tx
 constexpr int NDS = SCR / 8;            // 36 pieces per shortcut chunk
 constexpr int PATCH = NDP * 1024;
 constexpr int ROWB = PW * 128;
-constexpr int OFF_BIAS = 2 * PATCH;
-constexpr int SMEM = OFF_BIAS + 256 * 4;
+constexpr int SMEM = 2 * PATCH;
 constexpr int BAD = 0x7FFFFFF0;
 constexpr uint64_t KEY = 0xd92dad912240ull;  // variant 30's column key {0,0,1,1,2,2,4,4,5,5,6,6,2,2,6,6,0,0}
 static_assert(SMEM <= 160 * 1024, "LDS budget");
@@ -59,6 +58,19 @@ static_assert(SMEM <= 160 * 1024, "LDS budget");
 __device__ __forceinline__ int h31_key(int px) { return (int)((h31::KEY >> (3 * px)) & 7); }
 
 typedef unsigned int h31_v4 __attribute__((ext_vector_type(4)));
+typedef __bf16 h31_bf2 __attribute__((ext_vector_type(2)));
+typedef float h31_f2 __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair (RNE): one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t h31_pk(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((h31_f2){lo, hi}, h31_bf2));
+}
+// ReLU of a packed bf16 pair: as int16, negative bf16 values (and -0) are
+// negative, so max(x, 0) per half is relu (= relu before the rounding)
+__device__ __forceinline__ uint32_t h31_relu2(uint32_t x) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(x));
+  return r;
+}
 
 // BC channels per workgroup (256 or 128): NCG channel groups of 32 x NPG pixel
 // groups of TP tile rows
@@ -98,7 +110,8 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   const int ps0 = (int)a.in0_pstride * 2, ps1 = (int)a.in1_pstride * 2;
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   const int lrow = lane >> 3;
-  const int ab = a.ablate;  // timing ablations (wrong results): 1 no loads / DMA in the loop, 8 no epilogue
+  const int ab = a.ablate;  // timing ablations (wrong results): 1 no loads / DMA in the loop, 2 no patch DMA,
+                            // 4 no weight loads, 8 no epilogue
 
   // ---- weights: lane (fr, fg) of fragment (i, h) = row cw + i*16 + fr, K bytes
   // kb + h*64 + fg*16 of the step (kb = tap * cinb + chunk * 128)
@@ -154,10 +167,13 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
     }
   };
 
-  // ---- bias into LDS; prologue loads: the first chunk's patch, step 0's weights
-  float* s_bias = (float*)(smem + OFF_BIAS);
-  if (tid < BC / 4) *(float4*)(smem + OFF_BIAS + 16 * tid) = *(const float4*)(a.bias + c0 + 4 * tid);
+  // ---- prologue loads: the first chunk's patch, step 0's weights, the bias of
+  // this lane's channels (every tile's accumulators start at the bias: the
+  // epilogue adds nothing)
   issue_patch(tp_begin, 0, 0, -1);
+  f32x4 biasv[TC];
+#pragma unroll
+  for (int i = 0; i < TC; ++i) biasv[i] = *(const f32x4*)(a.bias + cw + i * 16 + fg * 4);
   // wnxt: the weights in flight (loaded one step ahead); wcur: this step's,
   // copied from wnxt only after the step's wait
   h31_v4 wcur[TC][2], wnxt[TC][2];
@@ -167,7 +183,7 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
 #pragma unroll
   for (int i = 0; i < TC; ++i)
 #pragma unroll
-    for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TP; ++j) acc[i][j] = biasv[i];
 
   // this step's weights: the copy from wnxt is where the compiler waits for
   // the loads (weights are compiler-tracked buffer loads; the patch DMA pieces,
@@ -214,21 +230,18 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   auto epilogue = [&](int t) __attribute__((always_inline)) {
     const int b = t / tiles_img, rem = t - b * tiles_img;
     const int oy0 = (rem / tiles_x) * TH, ox0 = (rem - (rem / tiles_x) * tiles_x) * TW;
-    float4 bias[TC];
-#pragma unroll
-    for (int i = 0; i < TC; ++i) bias[i] = *(const float4*)(s_bias + (cw - c0) + i * 16 + fg * 4);
     if constexpr (POOL) {
-      // the wave holds all 256 pixels of its channels: relu(acc + bias) summed
-      // over its 16 row fragments, then over the 16 lanes of a row (DPP)
+      // the wave holds all 256 pixels of its channels: relu(acc) (the bias is
+      // in acc) summed over its 16 row fragments, then over the 16 lanes of a
+      // row (DPP)
 #pragma unroll
       for (int i = 0; i < TC; ++i) {
-        const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
         float ps[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = 0.f;
 #pragma unroll
-          for (int j = 0; j < TP; ++j) v += fmaxf(acc[i][j][r] + bb[r], 0.f);
+          for (int j = 0; j < TP; ++j) v += fmaxf(acc[i][j][r], 0.f);
           ps[r] = row16_sum(v);
         }
         if (fr == 0)
@@ -236,29 +249,36 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
               make_float4(ps[0] * (1.f / 256), ps[1] * (1.f / 256), ps[2] * (1.f / 256), ps[3] * (1.f / 256));
       }
     } else {
+      // 16-B stores (the store tail is issue-bound): for fragment rows j, j+1
+      // one v_permlane16_swap per dword pairs lane row fg's 4 channels with its
+      // neighbour row's, so lane rows 0/2 hold 8 channels of pixel row j and
+      // rows 1/3 of row j + 1 (cdna_hip_programming.md T21, 16-lane form)
       u16* __restrict__ out = (u16*)a.out;
 #pragma unroll
-      for (int j = 0; j < TP; ++j) {
-        const int64_t px = (int64_t)(b * a.H + oy0 + r0w + j) * a.W + ox0 + fr;
+      for (int j = 0; j < TP; j += 2) {
+        const int64_t px = (int64_t)(b * a.H + oy0 + r0w + j + (fg & 1)) * a.W + ox0 + fr;
 #pragma unroll
         for (int i = 0; i < TC; ++i) {
-          const int co = cw + i * 16 + fg * 4;
-          float v[4] = {acc[i][j][0] + bias[i].x, acc[i][j][1] + bias[i].y, acc[i][j][2] + bias[i].z,
-                        acc[i][j][3] + bias[i].w};
+          const int co = cw + i * 16 + (fg >> 1) * 8;
+          uint32_t q[4] = {h31_pk(acc[i][j][0], acc[i][j][1]), h31_pk(acc[i][j][2], acc[i][j][3]),
+                           h31_pk(acc[i][j + 1][0], acc[i][j + 1][1]), h31_pk(acc[i][j + 1][2], acc[i][j + 1][3])};
           if (a.relu)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-          uint2 q;
-          q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *(uint2*)(out + px * a.out_pstride + co) = q;
+            for (int e = 0; e < 4; ++e) q[e] = h31_relu2(q[e]);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const auto r = __builtin_amdgcn_permlane16_swap(q[e], q[e + 2], false, false);
+            q[e] = r[0];
+            q[e + 2] = r[1];
+          }
+          *(uint4*)(out + px * a.out_pstride + co) = make_uint4(q[0], q[1], q[2], q[3]);
         }
       }
     }
 #pragma unroll
     for (int i = 0; i < TC; ++i)
 #pragma unroll
-      for (int j = 0; j < TP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < TP; ++j) acc[i][j] = biasv[i];
   };
 
   // ---- the K loop: tiles -> chunks -> steps.  Per step: wait for its weights;
@@ -279,7 +299,7 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
           // the chunk's patch pieces (this wave's); after a tile's epilogue its
           // stores (the youngest operations) may stay in flight
           if (post_epi)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(POOL ? 0 : TC * TP) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(POOL ? 0 : TC * TP / 2) : "memory");
           else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           post_epi = false;
@@ -291,8 +311,9 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
           // the next step's weights (after the last step: a harmless reload of
           // step 0's, so the wait counts stay uniform)
           const int kbn = tap + 1 < nsteps ? kb_of(c, tap + 1) : kb_of(ncn, 0);
-          load_w(kbn, wnxt);
-          if (sc) {
+          if (!(ab & 4)) load_w(kbn, wnxt);
+          if (ab & 2) {
+          } else if (sc) {
             issue_patch(nt, ncn, pbuf ^ 1, -1);  // waited for at the next step (a chunk start)
           } else if (tap >= 1 && tap <= 6) {
             issue_patch(nt, ncn, pbuf ^ 1, tap - 1);
@@ -336,7 +357,7 @@ int launch_halo256r(const BlockConvArgs& a, hipStream_t s) {
   SAD_REQUIRE((a.Cin * 2) % 128 == 0 && (!a.in1 || (a.Cin1 * 2) % 128 == 0), "variant 31: whole 128-B chunks");
   SAD_REQUIRE(!a.in1 || ((a.Ho - 1) * a.ss1 < a.H1 && (a.Wo - 1) * a.ss1 < a.W1), "variant 31: shortcut source");
   SAD_REQUIRE(a.wt_ld >= 9 * a.Cin + (a.in1 ? a.Cin1 : 0) && (a.wt_ld * 2) % 16 == 0, "variant 31: weight rows");
-  SAD_REQUIRE(a.out_pstride % 4 == 0 && a.in0_pstride % 8 == 0 && (!a.in1 || a.in1_pstride % 8 == 0),
+  SAD_REQUIRE(a.out_pstride % 8 == 0 && a.in0_pstride % 8 == 0 && (!a.in1 || a.in1_pstride % 8 == 0),
               "variant 31: pixel strides");
   SAD_REQUIRE(a.out || a.pool_out, "null output");
   SAD_REQUIRE(a.M == (int64_t)a.N * a.H * a.W, "variant 31: M = N H W");

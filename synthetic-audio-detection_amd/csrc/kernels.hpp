@@ -90,7 +90,7 @@ struct L1BlockArgs {
   int w2_ld;
   const float* b2;
   int64_t x_bytes;       // set by launch_l1block
-  int ablate;            // timing ablations (wrong results): 1 no patch DMA in the loop, 8 no epilogues
+  int ablate;            // reserved (0)
   uint64_t* stamps;      // diagnostic builds only (-DSAD_STAMPS): s_memtime per tile phase
 };
 int launch_l1block(const L1BlockArgs& a, hipStream_t s);

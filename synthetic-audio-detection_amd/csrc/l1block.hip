@@ -153,7 +153,6 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
   const __amdgpu_buffer_rsrc_t ro =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)a.x_bytes, 0x00020000);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  const int ab = a.ablate;  // timing ablation (wrong results): 1 no patch DMA in the loop
 
   // ---- patch piece k of this wave (q = wave + 4k: rows 8q .. 8q+7): the
   // lane's patch pixel (Y, X) and its source offset from the tile origin are
@@ -233,8 +232,9 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
   for (int t = tp_begin; t < tp_end; ++t) {
     stamp(t - tp_begin, 0);
     const bool has_next = t + 1 < tp_end;
+    // the next tile's patch (after the last tile: this tile's again, into the
+    // free buffer, which nothing reads -- no branch around the DMA)
     const TileO onext = tile_o(has_next ? t + 1 : t);
-    const bool dma_on = has_next && !(ab & 1);
     const int b = t / tiles_img, rem = t - b * tiles_img;
     const int ty = rem / tiles_x;
     const int oy0 = ty * 16, ox0 = (rem - ty * tiles_x) * 16;
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
       const uint4 bf = bq[u % DQ];
       if constexpr (u + DQ < NU1) bq[u % DQ] = rd1(std::integral_constant<int, u + DQ>{});
       if constexpr (u % 5 == 0 && u / 5 < QP)
-        if (dma_on) issue_piece(u / 5, onext, pb ^ 1);
+        issue_piece(u / 5, onext, pb ^ 1);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         if constexpr (s == 0)
