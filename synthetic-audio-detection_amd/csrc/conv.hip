@@ -463,6 +463,18 @@ constexpr int STEM_OPITCH = 160;                 // staging bytes per pooled pix
                                                  // 40 dwords -> the 4 rows a 32-lane group writes
                                                  // land on disjoint 8-bank sets
 
+// two floats -> packed bf16 pair (RNE): one v_cvt_pk_bf16_f32
+typedef __bf16 stem_bf2 __attribute__((ext_vector_type(2)));
+typedef float stem_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t stem_pk(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((stem_f2){lo, hi}, stem_bf2));
+}
+// ReLU of a packed bf16 pair (as int16 negative bf16 values are negative)
+__device__ __forceinline__ uint32_t stem_relu2(uint32_t x) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(x));
+  return r;
+}
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
@@ -665,10 +677,15 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
         for (int j = 0; j < 4; ++j) r[i][j] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
       return;
     }
+    // the plain bf16 stem starts the accumulators at the bias: max-pooling
+    // relu(x + b) is relu(max(x + b)), and the epilogue then adds nothing
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j) {
+        const float b0 = (!X3 && !TRAIN) ? s_bias[j * 16 + fr] : 0.f;
+        r[i][j] = f32x4{b0, b0, b0, b0};
+      }
     const int rb = 2 * (cr - 2 * py0) + 2;
     uint4 bw[4][2];  // weight fragments (LDS-resident; re-read per row keeps VGPRs for the pool)
     uint4 bwl[X3 ? 4 : 1][2];
@@ -769,6 +786,18 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
         const float send = fg == 3 ? (i > 0 ? cur[i - 1][j][3] : 0.f) : x[3];
         float left = __int_as_float(__builtin_amdgcn_ds_bpermute(((lane + 48) & 63) << 2, __float_as_int(send)));
         if (i == 0 && fg == 0) left = wave > 0 ? s_edge[(wave - 1) * 64 + j * 16 + fr] : -INFINITY;
+        if constexpr (!X3 && !TRAIN) {
+          // bias already in the accumulators: pooled pixels q0 = 32w+8i+2fg and
+          // q0 + 1 of channel c = 16j + fr packed as one bf16 pair, ReLU on the
+          // pair (int16 max), then lanes (c, c^1) trade pairs (one DPP) and a
+          // byte permute forms (c0, c0+1) of q0 (even lanes) / q0+1 (odd)
+          const uint32_t pq = stem_relu2(stem_pk(fmaxf(fmaxf(left, x[0]), x[1]), fmaxf(fmaxf(x[1], x[2]), x[3])));
+          const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pq, 0xB1, 0xF, 0xF, true);  // quad_perm 1,0,3,2
+          const uint32_t w = __builtin_amdgcn_perm(pn, pq, even ? 0x05040100u : 0x03020706u);
+          const int q = wave * 32 + i * 8 + 2 * fg + (even ? 0 : 1);
+          *(uint32_t*)(s_out + q * OPITCH + (j * 16 + (fr & ~1)) * 2) = w;
+          continue;
+        }
         const float oa = TRAIN ? fmaxf(fmaxf(left, x[0]), x[1]) : fmaxf(fmaxf(fmaxf(left, x[0]), x[1]) + bias[j], 0.f);
         const float ob = TRAIN ? fmaxf(fmaxf(x[1], x[2]), x[3]) : fmaxf(fmaxf(fmaxf(x[1], x[2]), x[3]) + bias[j], 0.f);
         const float oa_next = dppf<0x101>(oa);  // row_shl:1 (fr + 1)
