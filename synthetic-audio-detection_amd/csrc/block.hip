@@ -699,6 +699,7 @@ int launch_halo256(const BlockConvArgs& a, hipStream_t s, bool x3);
 int launch_halo256r(const BlockConvArgs& a, hipStream_t s);
 bool halo256_ok(const BlockConvArgs& a);
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s);
+int launch_l2conv(const BlockConvArgs& a, hipStream_t s);
 int launch_halo_rw_x3(const BlockConvArgs& a, hipStream_t s);
 
 // halo kernel (variant 20): bf16 stride-1 3x3 with Cout <= 128 (layer1, layer2's
@@ -734,6 +735,15 @@ static bool halo31_ok(const BlockConvArgs& a) {
   return a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Cout % 128 == 0 && a.H % 16 == 0 &&
          a.W % 16 == 0 && a.Ho == a.H && a.Wo == a.W && !a.res && !a.st_part && a.Cin % 64 == 0 &&
          (!a.in1 || a.Cin1 % 64 == 0) && (!a.pool_out || (a.H == 16 && a.W == 16 && a.Cout % 256 == 0));
+}
+// SAD_L2_RW=0 runs layer2's second block on the weight-ring halo kernel
+// (variant 20) instead of the resident-weight conv (variant 41; A/B switch)
+static bool l2_rw() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_L2_RW");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
 }
 bool layer2_halo() {
   static const bool v = [] {
@@ -804,6 +814,9 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
     return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   }
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
+  // layer2's second block (128 -> 128, stride 1, identity as an epilogue
+  // residual): the resident-weight conv (variant 41)
+  if (dtype == SAD_BF16 && l2_rw() && halo_ok(a, dtype) && a.Cin == 128 && a.Cout == 128 && !a.st_part) return 41;
   // layer2's 128-channel stride-1 convs (incl. conv2 + downsample / identity as
   // shortcut columns): variant 31 with 128-channel tiles
   if (dtype == SAD_BF16 && layer2_v31() && a.Cout == 128 && halo31_ok(a)) return 31;
@@ -848,6 +861,7 @@ static bool variant_fits(int v, int cout) {
   if (v == 20 || v == 21) return cout % 64 == 0;
   if (v == 22) return cout % 128 == 0;
   if (v == 25) return cout == 64;
+  if (v == 41) return cout == 128;
   return v >= 9 && v <= 19 && cout % bc[v] == 0;
 }
 
@@ -998,6 +1012,10 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   if (v == 31) {
     SAD_REQUIRE(dtype == SAD_BF16 && halo31_ok(a_in), "variant 31: bf16 3x3/s1/p1, Cout % 128, 16 x 16 tiles");
     return launch_halo256r(a, s);
+  }
+  if (v == 41) {
+    SAD_REQUIRE(dtype == SAD_BF16 && halo_ok(a_in, dtype), "variant 41: bf16 3x3/s1/p1, H, W % 16");
+    return launch_l2conv(a, s);
   }
   if (dtype == SAD_BF16X3 && v == 26) {
     SAD_REQUIRE(halo_ok(a_in, dtype), "split-bf16 halo conv: 3x3/s1/p1, H, W % 16");

@@ -67,6 +67,7 @@ struct BlockConvArgs {
   int Ho, Wo, Cout, relu;
   int64_t M;
   int64_t in0_bytes, in1_bytes, wt_bytes, res_bytes;  // set by launch_block_conv
+  int64_t out_bytes;     // (variant 41 sets it)
   int ablate;            // timing ablations (wrong results): 1 no DMA in loop, 2 no vmcnt wait, 4 no barrier,
                          // 8 no epilogue, 16 no weight DMA, 32 no patch DMA (halo)
   float* pool_out;       // optional fused global average pool, fp32 [N, Cout] (the variant's pixel tile

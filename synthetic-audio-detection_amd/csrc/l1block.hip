@@ -44,6 +44,7 @@
 #include "common.hpp"
 #include "igemm.hpp"
 #include "kernels.hpp"
+#include "rwconv.hpp"
 
 #include <stdio.h>
 
@@ -86,53 +87,6 @@ constexpr int l1b_k1(int u) { return u < SA * NF ? u % NF : (u - SA * NF) / NB1;
 }  // namespace l1b
 
 __device__ __forceinline__ int l1b_key(int x) { return (int)((l1b::KEY >> (3 * x)) & 7); }
-
-// acc (AGPR) [+]= w (AGPR) . b (VGPR)
-typedef unsigned int l1b_v4 __attribute__((ext_vector_type(4)));
-typedef unsigned int l1b_v2 __attribute__((ext_vector_type(2)));
-// acc (VGPR) [+]= w (AGPR) . b (VGPR).  hipcc places MFMA A/B operands only
-// in VGPRs, and the 288 weight registers of both convs do not fit there next
-// to the accumulators: the weights live in AGPRs, the MFMA is inline asm.
-__device__ __forceinline__ void l1b_mfma_a0(f32x4& acc, const l1b_v4& w, const uint4& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "a"(w), "v"(__builtin_bit_cast(l1b_v4, b)));
-}
-__device__ __forceinline__ void l1b_mfma_a(f32x4& acc, const l1b_v4& w, const uint4& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(__builtin_bit_cast(l1b_v4, b)));
-}
-// acc = c + w . b (the first K-step: C = the bias)
-__device__ __forceinline__ void l1b_mfma_ac(f32x4& acc, const l1b_v4& w, const uint4& b, const f32x4& c) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %3"
-               : "=&v"(acc)
-               : "a"(w), "v"(__builtin_bit_cast(l1b_v4, b)), "v"(c));
-}
-// the same with the weights in VGPRs (the AGPR file holds 256 of the 288)
-__device__ __forceinline__ void l1b_mfma_v0(f32x4& acc, const l1b_v4& w, const uint4& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(w), "v"(__builtin_bit_cast(l1b_v4, b)));
-}
-__device__ __forceinline__ void l1b_mfma_v(f32x4& acc, const l1b_v4& w, const uint4& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "v"(__builtin_bit_cast(l1b_v4, b)));
-}
-// two floats -> packed bf16 pair (RNE), one v_cvt_pk_bf16_f32
-typedef __bf16 l1b_bf2 __attribute__((ext_vector_type(2)));
-typedef float l1b_f2 __attribute__((ext_vector_type(2)));
-// relu of an asm MFMA result (fmaxf would first canonicalise it: one more VALU)
-__device__ __forceinline__ float l1b_relu(float x) {
-  float r;
-  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
-  return r;
-}
-__device__ __forceinline__ uint32_t l1b_pk(float lo, float hi) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((l1b_f2){lo, hi}, l1b_bf2));
-}
-
-template <typename F, int... I>
-__device__ __forceinline__ void l1b_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void l1b_for(F&& f) {
-  l1b_for_impl(f, std::make_integer_sequence<int, N>{});
-}
 
 __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
   using namespace l1b;
@@ -260,6 +214,17 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
       LYt[l] = min(8 * m + (frt >> 1), IWD - 1);
       LR0t[l] = (LYt[l] * PWD + 16 + et) * 128;
     }
+    // per-tile read bases: aligned (+ the patch buffer and the wave's row
+    // block), leftover (+ buffer) and the leftover row terms per tap row
+    int LAp[3], LRb[2], LYG[2][3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) LAp[kx] = LAt[kx] + pboa;
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      LRb[l] = LR0t[l] + pbo;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) LYG[l][ky] = ((LYt[l] + ky) & 3) << 1;
+    }
 
     // ---------------- conv1: 18 x 18 intermediate ----------------
     // Unit = one fragment read + its two MFMAs (channel tiles i = 0, 1).
@@ -277,11 +242,12 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
       if constexpr (k < NA) {
         const int Y = 9 * pg + k + ky;                       // uniform
         const int sg = ((Y & 3) << 5) ^ (h << 6);            // 2 (Y & 3) and the K-half, as chunk bits
-        return *(const uint4*)(smem + ((LAt[kx] ^ sg) + pboa) + (k + ky) * PROW);
+        // (pboa is a multiple of 128, so it commutes with the XOR on bits 4-6)
+        return *(const uint4*)(smem + (LAp[kx] ^ sg) + (k + ky) * PROW);
       } else {
         constexpr int l = k - NA;
-        const int pos = KXt[kx] ^ (((LYt[l] + ky) & 3) << 1) ^ (h << 2);
-        return *(const uint4*)(smem + (LR0t[l] + pbo + (pos << 4)) + (ky * PWD + kx) * 128);
+        const int pos = KXt[kx] ^ LYG[l][ky] ^ (h << 2);
+        return *(const uint4*)(smem + (LRb[l] + (pos << 4)) + (ky * PWD + kx) * 128);
       }
     };
     f32x4 b1v[2];
@@ -312,11 +278,11 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
         e1_addr = OFF_I + (y * IWD + x) * 128 + (((cw >> 3) + (fgt >> 1)) ^ l1b_key(x)) * 16 + (fgt & 1) * 8;
       }
       if constexpr ((part & 1) == 0) {
-        e1_qx = l1b_pk(l1b_relu(acc[i][k][0]), l1b_relu(acc[i][k][1])) & e1_inm;
+        e1_qx = l1b_relu2(l1b_pk(acc[i][k][0], acc[i][k][1])) & e1_inm;
       } else {
         uint2 q;
         q.x = e1_qx;
-        q.y = l1b_pk(l1b_relu(acc[i][k][2]), l1b_relu(acc[i][k][3])) & e1_inm;
+        q.y = l1b_relu2(l1b_pk(acc[i][k][2], acc[i][k][3])) & e1_inm;
         // channel tile 1 is chunk + 2: position (c + 2) ^ key = (c ^ key) ^ 2 (c even)
         *(uint2*)(smem + (i ? (e1_addr ^ 32) : e1_addr)) = q;
       }
@@ -405,11 +371,11 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
     auto epi2 = [&](auto jc, auto pc) __attribute__((always_inline)) {
       constexpr int jj = decltype(jc)::value, part = decltype(pc)::value, i = part >> 1;
       if constexpr ((part & 1) == 0) {
-        e2_qx = l1b_pk(l1b_relu(acc2[i][jj][0]), l1b_relu(acc2[i][jj][1]));
+        e2_qx = l1b_relu2(l1b_pk(acc2[i][jj][0], acc2[i][jj][1]));
       } else {
         uint2 q;
         q.x = e2_qx;
-        q.y = l1b_pk(l1b_relu(acc2[i][jj][2]), l1b_relu(acc2[i][jj][3]));
+        q.y = l1b_relu2(l1b_pk(acc2[i][jj][2], acc2[i][jj][3]));
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(l1b_v2, q), ro,
                                               (jj * a.W + fr2) * 128 + (cw + 16 * i + 4 * fg2) * 2, obase, 0);
       }

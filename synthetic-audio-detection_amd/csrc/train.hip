@@ -902,6 +902,7 @@ extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_
   // the patch-resident layer3/4 kernels (30, 31) sum no statistics; their
   // implicit-GEMM counterparts (13 / 15) do
   if ((v == 30 || v == 31) && dtype == SAD_BF16 && one_launch) v = gemm_block_variant(a);
+  if (v == 41 && dtype == SAD_BF16 && one_launch) v = 20;  // variant 41 sums no statistics either
   const bool fused = dtype == SAD_BF16 && one_launch && (v == 13 || v == 15 || v == 20 || v == 25);
   int rows = 0;
   if (fused) {

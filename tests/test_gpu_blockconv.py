@@ -88,6 +88,12 @@ CASES = [
     ('l2-id-31', 2, 64, 128, 128, 1, 'id', [31]),
     ('l2-ds-31', 2, 32, 64, 128, 1, 'ds', [31]),
     ('l3-two-tiles-31', 2, 16, 128, 384, 1, None, [31]),
+    # variant 41 (resident-weight 128 -> 128 conv, l2conv.hip): plain, with the
+    # epilogue residual, fewer tiles than workgroups (45), more (320)
+    ('l2-plain-41', 3, 64, 128, 128, 1, None, [41]),
+    ('l2-res-41', 2, 64, 128, 128, 1, 'res', [41]),
+    ('l2-res-41-ragged', 5, 48, 128, 128, 1, 'res', [41]),
+    ('l2-res-41-many', 20, 64, 128, 128, 1, 'res', [41]),
 ]
 
 
