@@ -745,6 +745,22 @@ static bool l2_rw() {
   }();
   return v;
 }
+// SAD_L2_DS_RW=0 runs layer2.0's conv2 + downsample on the implicit GEMM
+// (variant 15) instead of variant 41's downsample form (A/B switch)
+static bool l2_ds_rw() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_L2_DS_RW");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+// variant 41's downsample form: 128 -> 128 3x3/s1/p1 + 1x1/2 of a 64-channel
+// input at twice the size
+static bool l2conv_ds_ok(const BlockConvArgs& a) {
+  return a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Cin == 128 && a.Cout == 128 && a.H % 16 == 0 &&
+         a.W % 16 == 0 && a.Ho == a.H && a.Wo == a.W && a.in1 && a.Cin1 == 64 && a.ss1 == 2 && a.H1 == 2 * a.H &&
+         a.W1 == 2 * a.W && !a.res && !a.pool_out && !a.st_part;
+}
 bool layer2_halo() {
   static const bool v = [] {
     const char* e = getenv("SAD_L2_HALO");
@@ -817,6 +833,9 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   // layer2's second block (128 -> 128, stride 1, identity as an epilogue
   // residual): the resident-weight conv (variant 41)
   if (dtype == SAD_BF16 && l2_rw() && halo_ok(a, dtype) && a.Cin == 128 && a.Cout == 128 && !a.st_part) return 41;
+  // layer2's first block, conv2 + the downsample (its 1x1/2 of the 64-channel
+  // block input as two more K-steps): the same kernel
+  if (dtype == SAD_BF16 && l2_ds_rw() && l2conv_ds_ok(a)) return 41;
   // layer2's 128-channel stride-1 convs (incl. conv2 + downsample / identity as
   // shortcut columns): variant 31 with 128-channel tiles
   if (dtype == SAD_BF16 && layer2_v31() && a.Cout == 128 && halo31_ok(a)) return 31;
@@ -1014,7 +1033,7 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
     return launch_halo256r(a, s);
   }
   if (v == 41) {
-    SAD_REQUIRE(dtype == SAD_BF16 && halo_ok(a_in, dtype), "variant 41: bf16 3x3/s1/p1, H, W % 16");
+    SAD_REQUIRE(dtype == SAD_BF16 && (halo_ok(a_in, dtype) || l2conv_ds_ok(a_in)), "variant 41: bf16 3x3/s1/p1, H, W % 16");
     return launch_l2conv(a, s);
   }
   if (dtype == SAD_BF16X3 && v == 26) {

@@ -23,6 +23,12 @@
 // epilogue's 8-B reads are conflict-free).  149.5 KB.
 // Epilogue: bias already in the accumulators, + residual, ReLU on packed bf16,
 // 16-B stores (v_permlane16_swap pairs fragment rows j, j + 1).
+//
+// DS (layer2's first block, conv2 + downsample): the 1x1/2 downsample of the
+// 64-channel block input is two more K-steps after the conv's 36 (its weights
+// the 64 K columns behind the taps, 16 more VGPRs per wave), over a 16 x 16
+// pixel patch of the input at stride 2 DMA'd to LDS during chunk 0 (16-B chunk
+// c of pixel p at c ^ ((p >> 1) & 7): conflict-free fragment reads).
 #include "common.hpp"
 #include "igemm.hpp"
 #include "kernels.hpp"
@@ -39,6 +45,7 @@ constexpr int ROWB = PW * 128;
 constexpr int QP = (NDP + NW - 1) / NW;        // 11 pieces per wave per chunk
 constexpr int RESB = 256 * 256;                // residual tile: 256 pixels x 128 ch bf16
 constexpr int NRP = RESB / 1024 / NW;          // 16 residual pieces per wave
+constexpr int NDS = 256 * 128 / 1024 / NW;     // 8 downsample pieces per wave
 constexpr int OFF_RES = 2 * PATCH;
 constexpr int SMEM_RES = OFF_RES + RESB;
 constexpr int NS = 36;                         // K-steps: 2 chunks x 9 taps x 2 halves of 32 channels
@@ -53,8 +60,9 @@ static_assert(SMEM_RES + 512 <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ int l2c_key(int x) { return (int)((l2c::KEY >> (3 * x)) & 7); }
 
-template <bool RES>
+template <bool RES, bool DS>
 __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
+  static_assert(!(RES && DS), "one shortcut form");
   using namespace l2c;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -69,9 +77,8 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
 
   const __amdgpu_buffer_rsrc_t rx =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(RES ? a.res : a.in0), (short)0, (int)(RES ? a.res_bytes : 16),
-                                        0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(RES ? a.res : DS ? a.in1 : a.in0), (short)0, (int)(RES ? a.res_bytes : DS ? a.in1_bytes : 16), 0x00020000);
   const __amdgpu_buffer_rsrc_t ro =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)a.out_bytes, 0x00020000);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
@@ -118,6 +125,28 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
     dma16_m0(rr, off, lds0 + OFF_RES + q * 1024);
   };
 
+  // downsample piece k (q = wave + 4k: pixels 8q..8q+7 of the tile, 128 B
+  // each, source pixel (2 oy, 2 ox) of the 64-channel block input)
+  auto issue_ds = [&](int k, const TileO& o) __attribute__((always_inline)) {
+    const int q = wave + NW * k;
+    int ln;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    const int px = 8 * q + (ln >> 3), pos = ln & 7;
+    const int chunk = pos ^ ((px >> 1) & 7);
+    const int off = ((o.b * a.H1 + (o.oy0 + (px >> 4)) * a.ss1) * a.W1 + (o.ox0 + (px & 15)) * a.ss1) *
+                        (int)(a.in1_pstride * 2) + chunk * 16;
+    dma16_m0(rr, off, lds0 + OFF_RES + q * 1024);
+  };
+  // the downsample's weights: K-steps h = 0, 1 (channels (fg + 4h)*8..+7)
+  l1b_v4 wds[2][2];
+  if constexpr (DS) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        wds[i][h] = *(const l1b_v4*)((const u16*)a.wt + (size_t)(cw + 16 * i + fr) * a.wt_ld + 9 * 128 + (fg + 4 * h) * 8);
+  }
+
   // ---- weights into registers: K-step s = (chunk c, tap, half h) -> lane
   // (fr, fg) holds channels c*64 + (fg + 4h)*8 .. +7 of tap `tap` for output
   // channel cw + 16 i + fr
@@ -131,9 +160,9 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
                                   (fg + 4 * h) * 8);
     }
   // the bias (the accumulators' start value) behind the LDS buffers
-  if (tid < 32) *(float4*)(smem + (RES ? SMEM_RES : OFF_RES) + 16 * tid) = *(const float4*)(a.bias + 4 * tid);
+  if (tid < 32) *(float4*)(smem + (RES || DS ? SMEM_RES : OFF_RES) + 16 * tid) = *(const float4*)(a.bias + 4 * tid);
   auto biasv = [&](int i) __attribute__((always_inline)) {
-    return *(const f32x4*)(smem + (RES ? SMEM_RES : OFF_RES) + (cw + 16 * i + fg * 4) * 4);
+    return *(const f32x4*)(smem + (RES || DS ? SMEM_RES : OFF_RES) + (cw + 16 * i + fg * 4) * 4);
   };
   {
     const TileO o0 = tile_o(tp_begin);
@@ -201,6 +230,7 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
         // and residual (units 8, 24, ...); chunk 1 the next tile's chunk-0 patch
         if constexpr (u % 16 == 0 && u / 16 < QP) issue_piece(u / 16, c == 0 ? o : onext, c ^ 1);
         if constexpr (RES && c == 0 && u % 16 == 8 && u / 16 < NRP) issue_res(u / 16, o);
+        if constexpr (DS && c == 0 && u % 32 == 8 && u / 32 < NDS) issue_ds(u / 32, o);
         l1b_for<2>([&](auto ic) __attribute__((always_inline)) {
           constexpr int i = decltype(ic)::value;
           if constexpr (i == 1 && s >= NS - WV)
@@ -210,6 +240,25 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
         });
       });
     });
+    if constexpr (DS) {
+      // the downsample: 2 K-steps over the stride-2 input patch (published by
+      // the chunk-1 barrier, whose wait covered its pieces)
+      int ln;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+      const int frd = ln & 15, fgd = ln >> 4;
+      const int dbase = OFF_RES + frd * 128;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int dofs = dbase + ((((fgd + 4 * h) ^ ((frd >> 1) & 7))) << 4);
+        uint4 bd[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) bd[j] = *(const uint4*)(smem + dofs + j * 16 * 128);
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) l1b_mfma_v(acc[i][j], wds[i][h], bd[j]);
+      }
+    }
     // asm MFMA results read by compiler code: 12 wait states (8-pass XDL)
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 11" ::: "memory");
@@ -264,8 +313,11 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
 
 int launch_l2conv(const BlockConvArgs& a, hipStream_t s) {
   using namespace l2c;
-  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.in1 && !a.pool_out && !a.st_part,
-              "variant 41: 3x3/s1/p1, no GEMM shortcut, pool or statistics");
+  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.pool_out && !a.st_part,
+              "variant 41: 3x3/s1/p1, no pool or statistics");
+  SAD_REQUIRE(!a.in1 || (!a.res && a.Cin1 == 64 && a.ss1 == 2 && a.H1 == 2 * a.H && a.W1 == 2 * a.W &&
+                         a.in1_pstride % 8 == 0 && a.wt_ld >= 9 * 128 + 64),
+              "variant 41: the shortcut is a 1x1/2 downsample of a 64-channel input at twice the size");
   SAD_REQUIRE(a.Cin == 128 && a.Cout == 128, "variant 41: Cin = Cout = 128");
   SAD_REQUIRE(a.H % 16 == 0 && a.W % 16 == 0 && a.Ho == a.H && a.Wo == a.W, "variant 41: image must tile by 16 x 16");
   SAD_REQUIRE(a.wt_ld >= 9 * 128 && a.wt_ld % 8 == 0, "variant 41: weight rows");
@@ -282,19 +334,27 @@ int launch_l2conv(const BlockConvArgs& a, hipStream_t s) {
   if (a.res) {
     static bool attr = false;
     if (!attr) {
-      SAD_CHECK_HIP(hipFuncSetAttribute((const void*)l2conv_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        SMEM_RES + 512));
+      SAD_CHECK_HIP(hipFuncSetAttribute((const void*)l2conv_kernel<true, false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_RES + 512));
       attr = true;
     }
-    hipLaunchKernelGGL(l2conv_kernel<true>, dim3((unsigned)g), dim3(256), SMEM_RES + 512, s, b);
+    hipLaunchKernelGGL((l2conv_kernel<true, false>), dim3((unsigned)g), dim3(256), SMEM_RES + 512, s, b);
+  } else if (a.in1) {
+    static bool attr = false;
+    if (!attr) {
+      SAD_CHECK_HIP(hipFuncSetAttribute((const void*)l2conv_kernel<false, true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_RES + 512));
+      attr = true;
+    }
+    hipLaunchKernelGGL((l2conv_kernel<false, true>), dim3((unsigned)g), dim3(256), SMEM_RES + 512, s, b);
   } else {
     static bool attr = false;
     if (!attr) {
-      SAD_CHECK_HIP(hipFuncSetAttribute((const void*)l2conv_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        OFF_RES + 512));
+      SAD_CHECK_HIP(hipFuncSetAttribute((const void*)l2conv_kernel<false, false>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, OFF_RES + 512));
       attr = true;
     }
-    hipLaunchKernelGGL(l2conv_kernel<false>, dim3((unsigned)g), dim3(256), OFF_RES + 512, s, b);
+    hipLaunchKernelGGL((l2conv_kernel<false, false>), dim3((unsigned)g), dim3(256), OFF_RES + 512, s, b);
   }
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;

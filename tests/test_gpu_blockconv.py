@@ -94,6 +94,11 @@ CASES = [
     ('l2-res-41', 2, 64, 128, 128, 1, 'res', [41]),
     ('l2-res-41-ragged', 5, 48, 128, 128, 1, 'res', [41]),
     ('l2-res-41-many', 20, 64, 128, 128, 1, 'res', [41]),
+    # variant 41's downsample form (layer2.0's conv2 + the 1x1/2 of the
+    # 64-channel block input as two more K-steps)
+    ('l2-ds-41', 2, 64, 64, 128, 1, 'ds', [41]),
+    ('l2-ds-41-ragged', 5, 48, 64, 128, 1, 'ds', [41]),
+    ('l2-ds-41-many', 20, 64, 64, 128, 1, 'ds', [41]),
 ]
 
 
