@@ -700,6 +700,8 @@ int launch_halo256r(const BlockConvArgs& a, hipStream_t s);
 bool halo256_ok(const BlockConvArgs& a);
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s);
 int launch_l2conv(const BlockConvArgs& a, hipStream_t s);
+int launch_halo256s2(const BlockConvArgs& a, hipStream_t s);
+bool halo256s2_ok(const BlockConvArgs& a);
 int launch_halo_rw_x3(const BlockConvArgs& a, hipStream_t s);
 
 // halo kernel (variant 20): bf16 stride-1 3x3 with Cout <= 128 (layer1, layer2's
@@ -760,6 +762,20 @@ static bool l2conv_ds_ok(const BlockConvArgs& a) {
   return a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Cin == 128 && a.Cout == 128 && a.H % 16 == 0 &&
          a.W % 16 == 0 && a.Ho == a.H && a.Wo == a.W && a.in1 && a.Cin1 == 64 && a.ss1 == 2 && a.H1 == 2 * a.H &&
          a.W1 == 2 * a.W && !a.res && !a.pool_out && !a.st_part;
+}
+// SAD_S2_PATCH=1 runs the stride-2 3x3 convs (the first conv of layer2/3/4's
+// first block) on the patch-resident variant 32 (halo256s2.hip) instead of the
+// implicit GEMM (variants 13 / 15).  Off by default: measured same-box at mb
+// 512, l2.c1 644 vs 523 us, l3.c1 344 vs 328, l4.c1 284 vs 276, and -1.6 % end
+// to end; its ablations put 29-35 % of its time in the patch DMA (75 gathered
+// 1-KB pieces per 32-channel chunk) and 17-25 % in the epilogue.  Tested
+// (test_gpu_blockconv.py).
+static bool s2_patch() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_S2_PATCH");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return v;
 }
 bool layer2_halo() {
   static const bool v = [] {
@@ -847,6 +863,9 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   // micro-batch (a 1-rank and a 2-rank run of the same segments must agree
   // bit for bit)
   if (dtype == SAD_BF16 && halo256_mode() != 0 && halo256_ok(a)) return halo256_mode() == 2 ? 31 : 30;
+  // the stride-2 3x3 convs: the patch-resident variant 32 (chosen whatever the
+  // grid size, as above)
+  if (dtype == SAD_BF16 && s2_patch() && halo256s2_ok(a)) return 32;
   return gemm_block_variant(a);
 }
 // the implicit-GEMM choice (also the fused-statistics path's: 30/31 sum no
@@ -875,7 +894,7 @@ bool block_conv_can_pool(const BlockConvArgs& a, int dtype) {
 static bool variant_fits(int v, int cout) {
   if (v == 26) return cout == 64;
   if (v == 30) return cout % 256 == 0;
-  if (v == 31) return cout % 128 == 0;
+  if (v == 31 || v == 32) return cout % 128 == 0;
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128, 128};
   if (v == 20 || v == 21) return cout % 64 == 0;
   if (v == 22) return cout % 128 == 0;
@@ -1031,6 +1050,10 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   if (v == 31) {
     SAD_REQUIRE(dtype == SAD_BF16 && halo31_ok(a_in), "variant 31: bf16 3x3/s1/p1, Cout % 128, 16 x 16 tiles");
     return launch_halo256r(a, s);
+  }
+  if (v == 32) {
+    SAD_REQUIRE(dtype == SAD_BF16, "variant 32: bf16");
+    return launch_halo256s2(a, s);
   }
   if (v == 41) {
     SAD_REQUIRE(dtype == SAD_BF16 && (halo_ok(a_in, dtype) || l2conv_ds_ok(a_in)), "variant 41: bf16 3x3/s1/p1, H, W % 16");

@@ -99,6 +99,14 @@ CASES = [
     ('l2-ds-41', 2, 64, 64, 128, 1, 'ds', [41]),
     ('l2-ds-41-ragged', 5, 48, 64, 128, 1, 'ds', [41]),
     ('l2-ds-41-many', 20, 64, 64, 128, 1, 'ds', [41]),
+    # variant 32 (patch-resident stride-2 3x3, halo256s2.hip): layer2/3/4's
+    # first conv (128- and 256-channel tiles), few tiles (70 on 256
+    # workgroups), many (600 on 256)
+    ('l2-s2-32', 2, 128, 64, 128, 2, None, [32]),
+    ('l3-s2-32', 3, 64, 128, 256, 2, None, [32]),
+    ('l4-s2-32', 5, 32, 256, 512, 2, None, [32]),
+    ('l3-s2-32-ragged', 70, 32, 128, 256, 2, None, [32]),
+    ('l4-s2-32-many', 300, 32, 256, 512, 2, None, [32]),
 ]
 
 
