@@ -283,7 +283,7 @@ def main():
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'bf16x3', 'fp32'])
     ap.add_argument('--micro-batch', type=int, default=0,
                     help='segments per backbone launch sequence (0: 1024 bf16, 256 bf16x3, 128 fp32); stem/layer1 '
-                         'run in sub-batches of SAD_FRONT_MB=32, layers 2-4 on the whole micro-batch')
+                         'run in sub-batches of SAD_FRONT_MB (256 for bf16 with the fused layer1, else 32), layers 2-4 on the whole micro-batch')
     ap.add_argument('--parity-steps', type=int, default=0, help='timed steps of the bf16x3 parity mode '
                                                                 '(0: max(steps // 3, 3); -1: skip)')
     ap.add_argument('--fp32-steps', type=int, default=2, help='timed steps of the fp32 mode (N = 1; 0: skip)')

@@ -506,14 +506,16 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
 // With layer1 fused (bf16, variant 40) only the block inputs/outputs pass
 // through memory and the fused kernel's per-workgroup weight prologue wants
 // more tiles: 128 segments (+1.8-2.1 % end to end vs fused at 32, same box;
-// 64: +1.7-2 %).
+// 64: +1.7-2 %).  With layer2 on variant 41 (round 3): 256 is +0.4-3 % over 128
+// (same box, 3 rounds, tools/r03_sweep2.sh: 59.0-59.1k vs 57.3-58.9k seg/s;
+// 512 with micro-batch 2048 within 0.2 % of 256).
 static int front_sub_batch(int dtype) {
   static int v = [] {
     const char* e = getenv("SAD_FRONT_MB");
     return e ? atoi(e) : -1;
   }();
   if (v >= 0) return v;
-  return dtype == SAD_BF16 && l1_fused() ? 128 : 32;
+  return dtype == SAD_BF16 && l1_fused() ? 256 : 32;
 }
 
 static int run_chunk(const sad_backbone_plan* p, const float* map, const float* img, int64_t mb, float* feats,
