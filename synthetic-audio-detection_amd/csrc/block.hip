@@ -1007,8 +1007,11 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
     const int64_t imgr = a.res ? (int64_t)a.Ho * a.Wo * a.res_pstride * ES : 0;
     const int64_t imgo = (int64_t)a.Ho * a.Wo * a.out_pstride * ES;
     const int64_t per = std::max(img0, std::max(img1, imgr));
-    const int64_t nc = (lim - 65536) / per;
-    SAD_REQUIRE(nc >= 1, "one image exceeds the 2 GiB buffer range");
+    const int64_t ncap = (lim - 65536) / per;
+    SAD_REQUIRE(ncap >= 1, "one image exceeds the 2 GiB buffer range");
+    // equal ranges (1,024 images at 2 GiB + a bit: 512 + 512, not 1,023 + a
+    // 1-image launch whose grid is almost empty)
+    const int64_t nl = (a.N + ncap - 1) / ncap, nc = (a.N + nl - 1) / nl;
     for (int64_t n0 = 0; n0 < a.N; n0 += nc) {
       const int n = (int)std::min<int64_t>(nc, a.N - n0);
       BlockConvArgs c = a_in;  // logical channel counts (split-bf16 doubles them again)
