@@ -111,7 +111,7 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   const int lrow = lane >> 3;
   const int ab = a.ablate;  // timing ablations (wrong results): 1 no loads / DMA in the loop, 2 no patch DMA,
-                            // 4 no weight loads, 8 no epilogue
+                            // 4 no weight loads, 8 no epilogue, 128 no epilogue stores
 
   // ---- weights: lane (fr, fg) of fragment (i, h) = row cw + i*16 + fr, K bytes
   // kb + h*64 + fg*16 of the step (kb = tap * cinb + chunk * 128)
@@ -271,7 +271,11 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
             q[e] = r[0];
             q[e + 2] = r[1];
           }
-          *(uint4*)(out + px * a.out_pstride + co) = make_uint4(q[0], q[1], q[2], q[3]);
+          if (ab & 128) {  // timing: conversion + permutes kept, no store
+            asm volatile("" ::"v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[3]));
+          } else {
+            *(uint4*)(out + px * a.out_pstride + co) = make_uint4(q[0], q[1], q[2], q[3]);
+          }
         }
       }
     }
