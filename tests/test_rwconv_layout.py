@@ -1,0 +1,107 @@
+"""CPU: the LDS layouts of the layer2 resident-weight conv's downsample form
+(csrc/l2conv.hip, variant 41) and of the stride-2 patch kernel
+(csrc/halo256s2.hip, variant 32), checked exhaustively with the kernels' own
+index formulas.
+
+* every ds_read_b128 fragment read is free of LDS bank conflicts under the
+  MI355X ds_read_b128 lane grouping (MI355X_MICROARCH.md, LDS table: 4 groups
+  of 16 lanes, bank = (byte address / 4) mod 64), i.e. takes 4 LDS cycles;
+* the DMA's writer-side mapping (lane -> LDS slot, source pixel, source chunk)
+  and the readers' addressing agree: each lane reads the input pixel and the
+  8 channels its MFMA fragment needs;
+* variant 32's patch covers the 33 x 33 input window of a 16 x 16 output tile
+  at stride 2, and its padding slots are never read.
+"""
+GROUPS = [[0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27],
+          [4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31]]
+GROUPS += [[l + 32 for l in g] for g in GROUPS]
+
+
+def lds_cycles(addrs):
+    tot = 0
+    for g in GROUPS:
+        banks = {}
+        for l in g:
+            a = addrs[l]
+            for d in range(4):
+                banks.setdefault((a // 4 + d) % 64, set()).add(a)
+        tot += max(len(v) for v in banks.values())
+    return tot
+
+
+# ---- variant 41, downsample patch: pixel p of the 16 x 16 tile at p * 128 B,
+# 16-B chunk c at position c ^ ((p >> 1) & 7) (l2conv.hip issue_ds / DS reads)
+def ds_write_map():
+    """LDS byte offset -> (tile pixel, source chunk) as the DMA writes it:
+    piece q (8 pixels, 1 KB), lane ln writes 16 B at q * 1024 + ln * 16."""
+    m = {}
+    for q in range(32):
+        for ln in range(64):
+            px, pos = 8 * q + (ln >> 3), ln & 7
+            chunk = pos ^ ((px >> 1) & 7)
+            m[q * 1024 + ln * 16] = (px, chunk)
+    return m
+
+
+def test_l2conv_ds_reads_conflict_free_and_consistent():
+    wm = ds_write_map()
+    assert len(wm) == 256 * 8
+    for h in range(2):
+        for j in range(16):
+            addrs = []
+            for lane in range(64):
+                frd, fgd = lane & 15, lane >> 4
+                a = frd * 128 + (((fgd + 4 * h) ^ ((frd >> 1) & 7)) << 4) + j * 16 * 128
+                addrs.append(a)
+                # the lane needs pixel (row j, column frd), channels (fgd + 4h) * 8 .. + 7
+                assert wm[a] == (j * 16 + frd, fgd + 4 * h)
+            assert lds_cycles(addrs) == 4, (h, j)
+
+
+# ---- variant 32: patch row pitch 36 slots x 64 B; even input columns at slots
+# 0..16, odd at 20..35; chunk g of plane column c at g ^ key(c)
+PRW, ODD, NSLOT, KEYM = 36, 20, 33 * 36, 0xFE10
+
+
+def key32(c):
+    return ((KEYM >> c) & 1) << 1
+
+
+def s2_write_map():
+    """LDS byte offset -> (patch row, patch column x, source chunk) or None (zero pad)."""
+    m = {}
+    for q in range((NSLOT + 15) // 16):
+        for ln in range(64):
+            s = 16 * q + (ln >> 2)
+            row, col = s // PRW, s % PRW
+            odd = col >= ODD
+            lc = col - ODD if odd else col
+            x = 2 * lc + (1 if odd else 0)
+            ok = s < NSLOT and (odd or col <= 16)
+            m[q * 1024 + ln * 16] = (row, x, (ln & 3) ^ key32(lc)) if ok else None
+    return m
+
+
+def test_s2_patch_covers_window():
+    wm = s2_write_map()
+    got = {(r, x, c) for v in wm.values() if v is not None for (r, x, c) in [v]}
+    assert got == {(r, x, c) for r in range(33) for x in range(33) for c in range(4)}
+
+
+def test_s2_reads_conflict_free_and_consistent():
+    wm = s2_write_map()
+    for r0w in (0, 8):           # the two pixel halves of the 128-channel form
+        for ky in range(3):
+            for kx in range(3):
+                for j in range(16 - r0w):
+                    addrs = []
+                    for lane in range(64):
+                        fr, fg = lane & 15, lane >> 4
+                        lc = fr + (1 if kx == 2 else 0)
+                        slot = (ODD if kx == 1 else 0) + lc
+                        a = (2 * r0w + ky) * PRW * 64 + slot * 64 + ((fg ^ key32(lc)) << 4) + 2 * j * PRW * 64
+                        addrs.append(a)
+                        # output pixel (r0w + j, fr) at stride 2 reads input (2 (r0w + j) + ky, 2 fr + kx)
+                        # of the patch (origin at input (-1, -1) relative to the tile), channels fg * 8 .. + 7
+                        assert wm[a] == (2 * (r0w + j) + ky, 2 * fr + kx, fg), (r0w, ky, kx, j, lane)
+                    assert lds_cycles(addrs) == 4, (r0w, ky, kx, j)
