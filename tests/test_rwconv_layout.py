@@ -1,5 +1,6 @@
-"""CPU: the LDS layouts of the layer2 resident-weight conv's downsample form
-(csrc/l2conv.hip, variant 41) and of the stride-2 patch kernel
+"""CPU: the LDS layouts of the layer2 resident-weight conv (csrc/l2conv.hip,
+variant 41: its conv patch, residual tile and downsample patch) and of the
+stride-2 patch kernel
 (csrc/halo256s2.hip, variant 32), checked exhaustively with the kernels' own
 index formulas.
 
@@ -10,7 +11,9 @@ index formulas.
   and the readers' addressing agree: each lane reads the input pixel and the
   8 channels its MFMA fragment needs;
 * variant 32's patch covers the 33 x 33 input window of a 16 x 16 output tile
-  at stride 2, and its padding slots are never read.
+  at stride 2, and its padding slots are never read;
+* variant 41's residual reads (8-B halves, epilogue) fetch the 4 channels of
+  the accumulator fragment they are added to.
 """
 GROUPS = [[0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27],
           [4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31]]
@@ -105,3 +108,71 @@ def test_s2_reads_conflict_free_and_consistent():
                         # of the patch (origin at input (-1, -1) relative to the tile), channels fg * 8 .. + 7
                         assert wm[a] == (2 * (r0w + j) + ky, 2 * fr + kx, fg), (r0w, ky, kx, j, lane)
                     assert lds_cycles(addrs) == 4, (r0w, ky, kx, j)
+
+
+# ---- variant 41's conv patch (18 x 18 pixels of a 64-channel chunk, 128 B
+# each, chunk g at g ^ key(X): variant 30's column key) and its residual tile
+# (16 x 16 pixels x 256 B, chunk c at c ^ (px & 15), read as 8-B halves)
+KEY30 = 0xd92dad912240
+
+
+def key30(x):
+    return (KEY30 >> (3 * x)) & 7
+
+
+def test_l2conv_patch_reads_conflict_free_and_consistent():
+    wm = {}
+    for q in range(41):
+        for ln in range(64):
+            r = 8 * q + (ln >> 3)
+            if r < 18 * 18:
+                wm[q * 1024 + ln * 16] = (r // 18, r % 18, (ln & 7) ^ key30(r % 18))
+    for ky in range(3):
+        for kx in range(3):
+            for h in range(2):
+                for j in range(16):
+                    addrs = []
+                    for lane in range(64):
+                        frt, fgt = lane & 15, lane >> 4
+                        a = (((frt + kx) * 128 + ((fgt ^ key30(frt + kx)) << 4)) ^ (h << 6)) + (j + ky) * 18 * 128
+                        addrs.append(a)
+                        assert wm[a] == (j + ky, frt + kx, fgt + 4 * h)
+                    assert lds_cycles(addrs) == 4
+
+
+def lds_cycles_b64(addrs):
+    tot = 0
+    for g in (range(32), range(32, 64)):
+        banks = {}
+        for l in g:
+            a = addrs[l]
+            for d in range(2):
+                banks.setdefault((a // 4 + d) % 64, set()).add(a)
+        tot += max(len(v) for v in banks.values())
+    return tot
+
+
+def test_l2conv_residual_reads_consistent():
+    wm = {}
+    for q in range(64):
+        for ln in range(64):
+            px, pos = 4 * q + (ln >> 4), ln & 15
+            wm[q * 1024 + ln * 16] = (px, pos ^ (px & 15))
+    worst = 0
+    for wave in range(4):
+        cw = 32 * wave
+        for i in range(2):
+            for j in range(0, 16, 2):
+                for dj in range(2):
+                    addrs = []
+                    for lane in range(64):
+                        frt, fgt = lane & 15, lane >> 4
+                        ch = (cw >> 3) + 2 * i + (fgt >> 1)
+                        pa = (j + dj) * 16 + frt
+                        a = pa * 256 + ((ch ^ (pa & 15)) << 4) + (fgt & 1) * 8
+                        addrs.append(a)
+                        # 4 channels cw + 16 i + 4 fgt .. + 3 of pixel (j + dj, frt)
+                        px, chunk = wm[a - (fgt & 1) * 8]
+                        assert px == pa and chunk * 8 + (fgt & 1) * 4 == cw + 16 * i + 4 * fgt
+                    worst = max(worst, lds_cycles_b64(addrs))
+    assert worst <= 4  # 2 LDS cycles minimum for a b64 read; the epilogue's reads are off the MFMA path
