@@ -48,9 +48,11 @@ BF16_PEAK_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3        # f32 MFMA = f32 vector peak (MI355X_MICROARCH.md)
 # The dominant kernel and its rocprof key in the committed PMC traffic file
 # bf16: variant 31 (csrc/halo256r.hip), the 12 stride-1 layer3/4 convs of a
-# 2,048-segment step; the split-bf16 parity mode keeps variant 13 (all 16)
-DOMINANT_VARIANT = {'bf16': 31, 'bf16x3': 13, 'fp32': 13}
-DOMINANT_KERNEL = 'sad::halo256r_kernel<false>|131072'
+# 2,048-segment step; the split-bf16 parity mode runs its split form on the same convs
+DOMINANT_VARIANT = {'bf16': 31, 'bf16x3': 31, 'fp32': 13}
+# rocprof names the kernel with its template arguments ('sad::halo256r_kernel<256, false>|131072'); the
+# key is resolved by this name prefix (see dominant_traffic), so a template change cannot make it stale
+DOMINANT_KERNEL_PREFIX = 'sad::halo256r_kernel<'
 DOMINANT_DESC = ('sad::halo256r_kernel (variant 31): patch-resident 256-channel x 16x16-pixel conv, weights '
                  'streamed into registers; the 12 stride-1 layer3/4 convs of a step (stride-2 convs stay on the '
                  '256x256 implicit GEMM, variant 13)')
@@ -59,6 +61,20 @@ TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r03_pmc_traffi
 FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats
 FE_BYTES = 256000 + 128512     # int16 PCM read + fp32 [128, 251] map written
 HEADS = 6
+
+
+def dominant_traffic(tr: dict, prefix: str = DOMINANT_KERNEL_PREFIX):
+    """Memory-side bytes per launch (read + write) of the dominant kernel from a
+    committed PMC traffic file (tools/profile_bench.sh): the launch-weighted mean
+    over every record whose rocprof name starts with `prefix` (all template
+    instantiations, e.g. the pooled and plain forms of variant 31).  None when no
+    record matches or a matching record lacks its byte counts."""
+    recs = [v for k, v in tr.items() if k.startswith(prefix)]
+    if not recs or any(r.get('hbm_read_bytes') is None or r.get('hbm_write_bytes') is None for r in recs):
+        return None
+    w = [max(float(r.get('launches_per_step') or 1.0), 1e-9) for r in recs]
+    tot = sum(wi * (r['hbm_read_bytes'] + r['hbm_write_bytes']) for wi, r in zip(w, recs))
+    return round(tot / sum(w))
 
 
 def cpu_model() -> str:
@@ -358,10 +374,8 @@ def main():
         alg, exe, kinfo = kernel_roofline(r, fac)
         traffic = None
         if TRAFFIC_JSON and args.dtype == 'bf16':
-            tr = json.load(open(TRAFFIC_JSON))
-            rec = tr.get(DOMINANT_KERNEL)
-            if rec and rec.get('hbm_read_bytes') is not None:
-                traffic = rec['hbm_read_bytes'] + rec['hbm_write_bytes']
+            with open(TRAFFIC_JSON) as f:
+                traffic = dominant_traffic(json.load(f))
         bb_alg = BACKBONE_FLOP * B / (r['bb_ms'] * 1e-3) / 1e12
         out = {
             'metric': '4s@32kHz segments/sec end-to-end (mel+ResNet+ensemble), 1/2/4/8 MI355X',
@@ -405,7 +419,7 @@ def main():
                 'value': round(par['value'], 1), 'unit': 'segments/s', 'ms_per_step': round(par['ms'], 3),
                 'steps': p_steps, 'micro_batch': par_mode.mb,
                 'per_rank_ms_per_step': par['rank_ms_per_step'],
-                'roofline': {'kernel': 'block_conv_kernel variant 13, split-bf16', 'achieved': round(pexe, 1),
+                'roofline': {'kernel': 'halo256r_kernel (variant 31), split-bf16: the stride-1 layer3/4 convs', 'achieved': round(pexe, 1),
                              'unit': 'TFLOP/s (bf16 MFMA executed = 3 x algorithmic)', 'peak': BF16_PEAK_TFLOPS,
                              'frac': round(pexe / BF16_PEAK_TFLOPS, 4), 'algorithmic_tflops': round(palg, 1),
                              'algorithmic_frac_of_f32_peak': round(palg / F32_PEAK_TFLOPS, 4), **pinfo,

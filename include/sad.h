@@ -52,9 +52,11 @@ enum sad_dtype {
 /* ---------------------------------------------------------------- runtime */
 /* Select the device for this thread's subsequent plan creation. */
 int sad_init(int device);
-/* Wait for the device, then release what the library itself holds (the
- * launch-timing events of an unfinished sad_profile_begin).  Plans are
- * caller-owned: destroy them first.  sad_init may be called again after it. */
+/* Wait for the device, then release the launch-timing events of an
+ * unfinished sad_profile_begin.  The small per-device constant buffers the
+ * library allocates once (zero biases; stamp buffers of diagnostic builds) stay
+ * allocated until the process exits.  Plans are caller-owned: destroy them
+ * first.  sad_init may be called again after it. */
 int sad_shutdown(void);
 const char* sad_last_error(void);
 /* Library / kernel build identification (for provenance in bench output). */

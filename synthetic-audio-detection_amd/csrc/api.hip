@@ -461,7 +461,8 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
       b2.stride = 1;
       b2.wt_ld = 9 * blk.cout + blk.cin_sc;
       if ((p->dtype == SAD_BF16 || p->dtype == SAD_BF16X3) && blk.stride == 1 && Ho % 16 == 0 &&
-          (blk.cout <= 64 || (blk.cout <= 128 && layer2_halo() && !(p->dtype == SAD_BF16 && layer2_v31())))) {
+          (blk.cout <= 64 || (blk.cout <= 128 && layer2_halo() && !(p->dtype == SAD_BF16 && layer2_v31()) &&
+                            !(p->dtype == SAD_BF16X3 && x3_layer2_v31())))) {
         // identity blocks of layer1/2: the shortcut is an epilogue add on the halo kernel
         b2.res = bufA;
         b2.res_pstride = C;

@@ -696,7 +696,7 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
 
 int launch_halo_v(const BlockConvArgs& a, int v, hipStream_t s, bool x3 = false);
 int launch_halo256(const BlockConvArgs& a, hipStream_t s, bool x3);
-int launch_halo256r(const BlockConvArgs& a, hipStream_t s);
+int launch_halo256r(const BlockConvArgs& a, hipStream_t s, bool x3);
 bool halo256_ok(const BlockConvArgs& a);
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s);
 int launch_l2conv(const BlockConvArgs& a, hipStream_t s);
@@ -737,6 +737,17 @@ static bool halo31_ok(const BlockConvArgs& a) {
   return a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Cout % 128 == 0 && a.H % 16 == 0 &&
          a.W % 16 == 0 && a.Ho == a.H && a.Wo == a.W && !a.res && !a.st_part && a.Cin % 64 == 0 &&
          (!a.in1 || a.Cin1 % 64 == 0) && (!a.pool_out || (a.H == 16 && a.W == 16 && a.Cout % 256 == 0));
+}
+// SAD_X3_L2_V31 (split-bf16): layer2's stride-1 convs (layer2.0's conv2 +
+// downsample, layer2.1's two; identity / downsample as shortcut columns) on
+// variant 31's split form with 128-channel tiles instead of the weight-ring
+// halo kernel (variant 20) and the implicit GEMM (variant 15)
+bool x3_layer2_v31() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_X3_L2_V31");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
 }
 // SAD_L2_RW=0 runs layer2's second block on the weight-ring halo kernel
 // (variant 20) instead of the resident-weight conv (variant 41; A/B switch)
@@ -816,7 +827,7 @@ static bool x3_rw() {
 // The stride-1 3x3 convs with Cout % 256 == 0 (layer3/4): bf16 runs the
 // patch-resident variant 31 (weights streamed into registers, one barrier per
 // 64-channel chunk; 6-10 % faster than variant 13 per launch, +3 % end to end
-// same-box), split-bf16 the implicit GEMM (variant 13).  SAD_HALO256 (A/B
+// same-box), split-bf16 its split form too (round 4).  SAD_HALO256 (A/B
 // switch): 0 = variant 13 for both, 1 = variant 30 for both, 2 = the default.
 static int halo256_mode() {
   static const int v = [] {
@@ -842,7 +853,11 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   if (dtype == SAD_BF16X3) {
     // layer1 (64 -> 64): the resident-weight split-bf16 kernel (half the channels per workgroup)
     if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64 && x3_rw()) return 26;
+    if (x3_layer2_v31() && a.Cout == 128 && halo31_ok(a)) return 31;
     if (halo256_mode() == 1 && halo256_ok(a)) return 30;
+    // layer3/4 stride-1 convs: variant 31's split form (chosen whatever the
+    // grid size: its K order differs from variant 13's)
+    if (halo256_mode() == 2 && a.Cout % 256 == 0 && halo31_ok(a)) return 31;
     return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   }
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
@@ -1000,13 +1015,15 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   // single launch's, bit for bit); the fused-statistics launch, whose
   // per-workgroup rows would collide, is not split.
   const int64_t lim = (1ll << 31) - 65536;
-  if ((a.in0_bytes >= lim || a.in1_bytes >= lim || a.res_bytes >= lim) && a.N > 1 &&
+  // (the output too: variants 31 / 41 check it against the same range)
+  const int64_t out_bytes = a.out ? ((a.M - 1) * a.out_pstride + a.Cout) * ES : 0;
+  if ((a.in0_bytes >= lim || a.in1_bytes >= lim || a.res_bytes >= lim || out_bytes >= lim) && a.N > 1 &&
       a.M == (int64_t)a.N * a.Ho * a.Wo && !a.st_part) {
     const int64_t img0 = (int64_t)a.H * a.W * a.in0_pstride * ES;
     const int64_t img1 = a.in1 ? (int64_t)a.H1 * a.W1 * a.in1_pstride * ES : 0;
     const int64_t imgr = a.res ? (int64_t)a.Ho * a.Wo * a.res_pstride * ES : 0;
     const int64_t imgo = (int64_t)a.Ho * a.Wo * a.out_pstride * ES;
-    const int64_t per = std::max(img0, std::max(img1, imgr));
+    const int64_t per = std::max(std::max(img0, imgo), std::max(img1, imgr));
     const int64_t ncap = (lim - 65536) / per;
     SAD_REQUIRE(ncap >= 1, "one image exceeds the 2 GiB buffer range");
     // equal ranges (1,024 images at 2 GiB + a bit: 512 + 512, not 1,023 + a
@@ -1051,8 +1068,9 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
 #endif
   }
   if (v == 31) {
-    SAD_REQUIRE(dtype == SAD_BF16 && halo31_ok(a_in), "variant 31: bf16 3x3/s1/p1, Cout % 128, 16 x 16 tiles");
-    return launch_halo256r(a, s);
+    SAD_REQUIRE((dtype == SAD_BF16 || dtype == SAD_BF16X3) && halo31_ok(a_in),
+                "variant 31: bf16 / split-bf16 3x3/s1/p1, Cout % 128, 16 x 16 tiles");
+    return launch_halo256r(a, s, dtype == SAD_BF16X3);
   }
   if (v == 32) {
     SAD_REQUIRE(dtype == SAD_BF16, "variant 32: bf16");

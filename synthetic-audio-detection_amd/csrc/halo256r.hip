@@ -73,8 +73,14 @@ __device__ __forceinline__ uint32_t h31_relu2(uint32_t x) {
 }
 
 // BC channels per workgroup (256 or 128): NCG channel groups of 32 x NPG pixel
-// groups of TP tile rows
-template <int BC, bool POOL>
+// groups of TP tile rows.
+// X3: split-bf16 parity mode (block.hip's layout: a 128-B chunk holds 32 logical
+// channels, bytes 0-63 hi = bf16(v), 64-127 lo = bf16(v - hi), for pixels and
+// weights alike).  A K-step's two halves then run W_hi.X_hi + W_lo.X_hi (half 0,
+// both weight halves on the hi fragment) + W_hi.X_lo (half 1): 96 MFMAs per
+// K-step and wave on the same operand reads and weight loads as bf16's 64; the
+// epilogue splits the fp32 result into hi / lo again.
+template <int BC, bool POOL, bool X3 = false>
 __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   using namespace h31;
   constexpr int NCG = BC / 32, NPG = NW / NCG, TP = 16 / NPG;
@@ -206,8 +212,11 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
     const int o1 = (kx + fr) * 128 + (((fg + 4) ^ h31_key(kx + fr)) << 4);
     const char* pb0 = smem + pbase + o0;
     const char* pb1 = smem + pbase + o1;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    auto half = [&](auto hc) __attribute__((always_inline)) {
+      constexpr int h = decltype(hc)::value;
+      // bf16: W_h.X_h.  Split-bf16, half 0 (the hi fragment): W_hi.X_hi and
+      // W_lo.X_hi; half 1 (the lo fragment): W_hi.X_lo.
+      constexpr int NM = X3 && h == 0 ? 2 : 1;  // weight halves per fragment
       const char* pb = h ? pb1 : pb0;
       uint4 bf[TP];
 #pragma unroll
@@ -215,16 +224,21 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
 #pragma unroll
       for (int j = 0; j < TP; ++j)
 #pragma unroll
-        for (int i = 0; i < TC; ++i) mfma_chunk<u16>(__builtin_bit_cast(uint4, wcur[i][h]), bf[j], acc[i][j]);
+        for (int m = 0; m < NM; ++m)
+#pragma unroll
+          for (int i = 0; i < TC; ++i)
+            mfma_chunk<u16>(__builtin_bit_cast(uint4, wcur[i][X3 ? m : h]), bf[j], acc[i][j]);
       // reads run 4 fragments ahead of the MFMAs that consume them
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
       for (int j = 0; j < TP - 4; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x008, TC, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NM * TC, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4 * TC, 0);
-    }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * NM * TC, 0);
+    };
+    half(std::integral_constant<int, 0>{});
+    half(std::integral_constant<int, 1>{});
   };
 
   auto epilogue = [&](int t) __attribute__((always_inline)) {
@@ -259,6 +273,37 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
         const int64_t px = (int64_t)(b * a.H + oy0 + r0w + j + (fg & 1)) * a.W + ox0 + fr;
 #pragma unroll
         for (int i = 0; i < TC; ++i) {
+          if constexpr (X3) {
+            // ReLU in fp32, then hi = bf16(v), lo = bf16(v - hi) (block.hip's
+            // split); hi and lo go to the two 32-channel halves of the wave's
+            // 128-B output chunk (cw is a multiple of 32)
+            float v[2][4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[0][r] = a.relu ? fmaxf(acc[i][j][r], 0.f) : acc[i][j][r];
+              v[1][r] = a.relu ? fmaxf(acc[i][j + 1][r], 0.f) : acc[i][j + 1][r];
+            }
+            uint32_t qh[4], ql[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x0 = v[e >> 1][2 * (e & 1)], x1 = v[e >> 1][2 * (e & 1) + 1];
+              qh[e] = h31_pk(x0, x1);
+              ql[e] = h31_pk(x0 - __uint_as_float(qh[e] << 16), x1 - __uint_as_float(qh[e] & 0xFFFF0000u));
+            }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const auto rh = __builtin_amdgcn_permlane16_swap(qh[e], qh[e + 2], false, false);
+              qh[e] = rh[0];
+              qh[e + 2] = rh[1];
+              const auto rl = __builtin_amdgcn_permlane16_swap(ql[e], ql[e + 2], false, false);
+              ql[e] = rl[0];
+              ql[e + 2] = rl[1];
+            }
+            u16* op = out + px * a.out_pstride + 2 * cw + i * 16 + (fg >> 1) * 8;
+            *(uint4*)op = make_uint4(qh[0], qh[1], qh[2], qh[3]);
+            *(uint4*)(op + 32) = make_uint4(ql[0], ql[1], ql[2], ql[3]);
+            continue;
+          }
           const int co = cw + i * 16 + (fg >> 1) * 8;
           uint32_t q[4] = {h31_pk(acc[i][j][0], acc[i][j][1]), h31_pk(acc[i][j][2], acc[i][j][3]),
                            h31_pk(acc[i][j + 1][0], acc[i][j + 1][1]), h31_pk(acc[i][j + 1][2], acc[i][j + 1][3])};
@@ -303,7 +348,7 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
           // the chunk's patch pieces (this wave's); after a tile's epilogue its
           // stores (the youngest operations) may stay in flight
           if (post_epi)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(POOL ? 0 : TC * TP / 2) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(POOL ? 0 : (X3 ? 2 : 1) * TC * TP / 2) : "memory");
           else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           post_epi = false;
@@ -334,12 +379,12 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BC, bool POOL>
+template <int BC, bool POOL, bool X3>
 static int launch_halo256r_t(const BlockConvArgs& a, hipStream_t s) {
   using namespace h31;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)halo256r_kernel<BC, POOL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)halo256r_kernel<BC, POOL, X3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               SMEM);
     attr = true;
   }
@@ -347,13 +392,15 @@ static int launch_halo256r_t(const BlockConvArgs& a, hipStream_t s) {
   const int64_t tiles_p = (int64_t)a.N * (a.H / TH) * (a.W / TW);
   int64_t g = std::min<int64_t>(tiles_p * n_tc, 256);
   g = std::max<int64_t>(n_tc, g / n_tc * n_tc);
-  hipLaunchKernelGGL((halo256r_kernel<BC, POOL>), dim3((unsigned)g), dim3(512), SMEM, s, a);
+  hipLaunchKernelGGL((halo256r_kernel<BC, POOL, X3>), dim3((unsigned)g), dim3(512), SMEM, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }
 
-// (a: the kernel's bf16 channel counts and strides, as launch_block_conv passes them)
-int launch_halo256r(const BlockConvArgs& a, hipStream_t s) {
+// (a: the kernel's bf16 channel counts and strides, as launch_block_conv passes
+// them; x3: the split-bf16 layout, Cin / Cin1 / strides / wt_ld already doubled,
+// Cout and the bias logical)
+int launch_halo256r(const BlockConvArgs& a, hipStream_t s, bool x3) {
   SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1, "variant 31: 3x3, stride 1, pad 1");
   SAD_REQUIRE(!a.res && !a.st_part, "variant 31: no epilogue residual / fused statistics (shortcut as in1)");
   SAD_REQUIRE(a.Cout % 128 == 0, "variant 31: Cout must be a multiple of 128");
@@ -368,9 +415,11 @@ int launch_halo256r(const BlockConvArgs& a, hipStream_t s) {
   if (a.pool_out) {
     SAD_REQUIRE(a.H == 16 && a.W == 16 && a.Cout % 256 == 0,
                 "variant 31 fused average pool: a 16 x 16 tile must be one image, Cout % 256");
-    return launch_halo256r_t<256, true>(a, s);
+    return x3 ? launch_halo256r_t<256, true, true>(a, s) : launch_halo256r_t<256, true, false>(a, s);
   }
-  return a.Cout % 256 == 0 ? launch_halo256r_t<256, false>(a, s) : launch_halo256r_t<128, false>(a, s);
+  if (x3)
+    return a.Cout % 256 == 0 ? launch_halo256r_t<256, false, true>(a, s) : launch_halo256r_t<128, false, true>(a, s);
+  return a.Cout % 256 == 0 ? launch_halo256r_t<256, false, false>(a, s) : launch_halo256r_t<128, false, false>(a, s);
 }
 
 }  // namespace sad

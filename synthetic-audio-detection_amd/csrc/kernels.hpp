@@ -123,7 +123,8 @@ int launch_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, int vari
 int default_block_variant(const BlockConvArgs& a, int dtype);
 int gemm_block_variant(const BlockConvArgs& a);  // default_block_variant without 30/31 (bf16)
 bool layer2_halo();
-bool layer2_v31();  // SAD_L2_V31 (default 1): layer2's stride-1 convs on variant 31 (128-channel tiles)
+bool x3_layer2_v31();  // SAD_X3_L2_V31 (default 1): split-bf16 layer2 stride-1 convs on variant 31 (128-channel tiles)
+bool layer2_v31();  // SAD_L2_V31 (default 0; 1: measured 2.2-2.7 % slower): layer2's stride-1 convs on variant 31 (128-channel tiles)
 bool block_conv_can_pool(const BlockConvArgs& a, int dtype);  // default variant pools Ho x Wo tiles  // SAD_L2_HALO (default 1): layer2's identity blocks on the halo kernel
 // dx (+)= col2im(dcol) (train.hip; the strided dgrad of wgrad.hip)
 int launch_col2im(const float* dcol, int64_t N, int H, int W, int C, int k, int stride, int pad, int Ho, int Wo,

@@ -29,10 +29,14 @@
 //
 // LDS (144 KB): 2 x input patch [20 x 20 pixels][128 B] (the next tile's patch
 // is DMA'd during this tile's conv1, one piece per K-step), the intermediate
-// [18 x 18][128 B] and the biases.  Swizzles (16-B chunk c of a pixel row):
-//  * intermediate row (y, x): position c ^ key(x)  -- variant 30's column key,
-//    conflict-free for row-aligned fragments at every tap column, so conv2's
-//    fragment address is a lane constant + an immediate row offset;
+// [18 rows][18 x 128 B + 16 B pad] and the biases.  Swizzles (16-B chunk c of a
+// pixel):
+//  * intermediate pixel (y, x): position c ^ key(x) -- a column key that is
+//    conflict-free for row-aligned fragment reads at every tap column (conv2's
+//    fragment address is a lane constant + an immediate row offset) and takes
+//    each value twice over columns 0-15 (conv1's aligned 8-B stores: 2-way);
+//    the 16-B row pad staggers the 8 rows of a leftover fragment's stores over
+//    the bank space (2-way; 8-way without it);
 //  * patch row (Y, X): position c ^ key(X) ^ 2 (Y & 3) -- the row term is
 //    uniform over an aligned fragment (an XOR with a scalar keeps it
 //    conflict-free) and spreads the leftover fragments' 4 rows per column
@@ -60,11 +64,13 @@ namespace sad {
 namespace l1b {
 constexpr int NW = 4;                      // waves: one per SIMD
 constexpr int PWD = 20, PR = PWD * PWD;    // input patch 20 x 20 (halo 2)
-constexpr int IWD = 18, IR = IWD * IWD;    // intermediate 18 x 18 (halo 1)
+constexpr int IWD = 18;                       // intermediate 18 x 18 (halo 1)
 constexpr int PATCH = PR * 128;            // 51,200 B
-constexpr int PROW = PWD * 128, IROW = IWD * 128;
+// intermediate row pitch: 18 pixels + 16 B, so consecutive rows start 16 B
+// apart in the bank space (the leftover fragments' stores span 8 rows)
+constexpr int PROW = PWD * 128, IROW = IWD * 128 + 16;
 constexpr int OFF_I = 2 * PATCH;           // patches double-buffered
-constexpr int OFF_B = OFF_I + IR * 128;    // b1 [64], b2 [64] fp32
+constexpr int OFF_B = OFF_I + IWD * IROW;  // b1 [64], b2 [64] fp32
 constexpr int SMEM = OFF_B + 2 * 64 * 4;
 constexpr int NDP = PR / 8;                // 50 DMA pieces of 8 pixel rows
 constexpr int QP = (NDP + NW - 1) / NW;    // 13 per wave (waves 2, 3: 12)
@@ -78,7 +84,11 @@ constexpr int SA = 6;                      // conv1 K-steps run K-step-outer (th
 constexpr int NB1 = NS - SA;
 constexpr int W2V = 8;                     // conv2 K-steps of channel tile 1 whose weights sit in VGPRs
 constexpr int BAD = 0x7FFFFFF0;
-constexpr uint64_t KEY = 0xd92dad912240ull;  // variant 30's column key (columns 18, 19: 0)
+// column key {0,0,1,1,2,3,4,4,5,5,6,7,2,3,6,7,0,0} (columns 18, 19: 0): every
+// fragment read conflict-free (as variant 30's key), and over columns 0-15
+// each value exactly twice, so conv1's aligned 8-B intermediate stores are
+// 2-way (the ds_write_b64 minimum for 128-B pixels; variant 30's key: 4-way)
+constexpr uint64_t KEY = 0xf9afad91a240ull;
 static_assert(SMEM <= 160 * 1024, "LDS budget");
 static_assert(NDP % 2 == 0, "pieces");
 // conv1 unit u -> (K-step, fragment): phase A K-step-outer, phase B fragment-outer
@@ -261,7 +271,7 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
     // epilogue of fragment k in 4 parts (channel tile i = part / 2; first or
     // second half of the 4 values), so it can be spread between MFMAs
     uint32_t e1_inm = 0, e1_qx = 0;
-    int e1_addr = 0;
+    int e1_addr = 0, e1_addr1 = 0;
     auto epi1 = [&](auto kc, auto pc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value, part = decltype(pc)::value, i = part >> 1;
       if constexpr (part == 0) {
@@ -275,7 +285,13 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
           x = 16 + et;
           e1_inm = (unsigned)(oy0 - 1 + y) < (unsigned)a.H ? cml : 0u;
         }
-        e1_addr = OFF_I + (y * IWD + x) * 128 + (((cw >> 3) + (fgt >> 1)) ^ l1b_key(x)) * 16 + (fgt & 1) * 8;
+        // channel tile 1 is chunk + 2: position (c + 2) ^ key = (c ^ key) ^ 2 (c
+        // even); the XOR stays inside the pixel (the padded row pitch is not a
+        // multiple of 64 B)
+        const int pix = OFF_I + y * IROW + x * 128;
+        const int pos = (((cw >> 3) + (fgt >> 1)) ^ l1b_key(x)) * 16 + (fgt & 1) * 8;
+        e1_addr = pix + pos;
+        e1_addr1 = pix + (pos ^ 32);
       }
       if constexpr ((part & 1) == 0) {
         e1_qx = l1b_relu2(l1b_pk(acc[i][k][0], acc[i][k][1])) & e1_inm;
@@ -283,8 +299,7 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
         uint2 q;
         q.x = e1_qx;
         q.y = l1b_relu2(l1b_pk(acc[i][k][2], acc[i][k][3])) & e1_inm;
-        // channel tile 1 is chunk + 2: position (c + 2) ^ key = (c ^ key) ^ 2 (c even)
-        *(uint2*)(smem + (i ? (e1_addr ^ 32) : e1_addr)) = q;
+        *(uint2*)(smem + (i ? e1_addr1 : e1_addr)) = q;
       }
     };
     uint4 bq[DQ];
@@ -308,8 +323,14 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
       // distance; the asm MFMAs keep compiler code from moving across them)
       if constexpr (u >= SA * NF && k >= 1) {
         constexpr int q = (u - SA * NF) % NB1;
-        if constexpr (q >= 2 && q <= 8 && q % 2 == 0)
+        if constexpr (q >= 2 && q <= 8 && q % 2 == 0) {
+          // pinned between the MFMAs: the asm MFMAs' results have no hazard
+          // tracking, so the scheduler must not hoist these reads of acc
+          // toward the MFMA that wrote it
+          __builtin_amdgcn_sched_barrier(0);
           epi1(std::integral_constant<int, k - 1>{}, std::integral_constant<int, q / 2 - 1>{});
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     });
     stamp(t - tp_begin, 1);
@@ -396,10 +417,17 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
       });
       // fragment jj-1's epilogue parts after units 2, 4, 6, 8 of fragment jj,
       // fragment jj+1's accumulator init after units 10 and 12
-      if constexpr (jj >= 1 && s >= 2 && s <= 8 && s % 2 == 0)
+      // (pinned between the MFMAs, as conv1's epilogue parts)
+      if constexpr (jj >= 1 && s >= 2 && s <= 8 && s % 2 == 0) {
+        __builtin_amdgcn_sched_barrier(0);
         epi2(std::integral_constant<int, jj - 1>{}, std::integral_constant<int, s / 2 - 1>{});
-      if constexpr (jj + 1 < 8 && (s == 10 || s == 12))
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (jj + 1 < 8 && (s == 10 || s == 12)) {
+        __builtin_amdgcn_sched_barrier(0);
         init2(std::integral_constant<int, jj + 1>{}, std::integral_constant<int, (s - 10) / 2>{});
+        __builtin_amdgcn_sched_barrier(0);
+      }
     });
     stamp(t - tp_begin, 3);
     __builtin_amdgcn_sched_barrier(0);

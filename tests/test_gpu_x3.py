@@ -46,6 +46,16 @@ def _conv_ref(x, w, stride, pad, sc=None, wsc=None, sc_stride=1, bias=None, relu
     (128, 256, 32, 2, 'downsample', 30),
     (256, 512, 32, 1, None, 30),
     (128, 128, 16, 1, None, 10),
+    # variant 31's split form (halo256r.hip, round 4): the layer3/4 stride-1 default
+    (256, 256, 16, 1, 'identity', 31),
+    (256, 256, 32, 1, 'identity', 31),
+    (128, 256, 32, 2, 'downsample', 31),
+    (256, 512, 32, 1, None, 31),
+    (512, 512, 16, 1, 'identity', 31),
+    # ... and its 128-channel tiles (layer2's stride-1 convs in the parity mode)
+    (128, 128, 16, 1, 'identity', 31),
+    (64, 128, 32, 2, 'downsample', 31),
+    (128, 128, 48, 1, None, 31),
 ])
 def test_block_conv_x3_vs_float64(cin, cout, H, stride, shortcut, variant):
     from sad.engine import block_conv, from_split, to_split
