@@ -459,9 +459,15 @@ constexpr int STEM_BPITCH = 544;                 // bf16 elements per band row (
 constexpr int STEM_HROWS = 12;                   // x-interpolated map rows kept in LDS (>= 4P+8 image rows at 128/512)
 constexpr int STEM_UPITCH = 520;                 // floats per x-interpolated row, indexed by band column
                                                  // (>= 518 read; zero outside the image)
-constexpr int STEM_OPITCH = 160;                 // staging bytes per pooled pixel (64 ch bf16 + pad):
-                                                 // 40 dwords -> the 4 rows a 32-lane group writes
-                                                 // land on disjoint 8-bank sets
+constexpr int STEM_OPITCH = 128;                 // staging bytes per pooled pixel (64 ch bf16), 16-B
+                                                 // chunk c of pixel q at c ^ stem_oswz(q)
+constexpr int STEM_WPITCH = 80;                  // bf16 per weight row in LDS (64 + pad): the
+                                                 // fragment reads are conflict-free (72: 2-way)
+// pooled-row staging swizzle (bf16 stems): chunk c of pixel q at c ^ g(q), g =
+// 0, 4, 2, 6 for q mod 4 -- the b32 stores of a 32-lane group (4 pixels x 2
+// chunks) and the b128 row copy-out are both conflict-free (a padded pitch
+// cannot do both: 160 B gave 3-way reads)
+__device__ __forceinline__ int stem_oswz(int q) { return ((q & 1) << 2) | (q & 2); }
 
 // two floats -> packed bf16 pair (RNE): one v_cvt_pk_bf16_f32
 typedef __bf16 stem_bf2 __attribute__((ext_vector_type(2)));
@@ -511,8 +517,8 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
   constexpr int OPITCH = X3 ? STEM_OPITCH_X3 : STEM_OPITCH;
   __shared__ __attribute__((aligned(16))) u16 s_img[STEM_BAND_ROWS * STEM_BPITCH];
   __shared__ __attribute__((aligned(16))) u16 s_imgl[X3 ? STEM_BAND_ROWS * STEM_BPITCH : 8];
-  __shared__ __attribute__((aligned(16))) u16 s_w[64 * 72];
-  __shared__ __attribute__((aligned(16))) u16 s_wl[X3 ? 64 * 72 : 8];
+  __shared__ __attribute__((aligned(16))) u16 s_w[64 * STEM_WPITCH];
+  __shared__ __attribute__((aligned(16))) u16 s_wl[X3 ? 64 * STEM_WPITCH : 8];
   __shared__ __attribute__((aligned(16))) float s_bias[64];
   // x-interpolated map rows while the band is built; afterwards the pooled-row
   // staging [128 q][64 ch] bf16 (X3: hi + lo) and the wave-edge exchange [4][64] fp32
@@ -523,12 +529,13 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int py0 = blockIdx.x * STEM_P;
   const int64_t b = blockIdx.y;
-  for (int i = tid; i < 64 * 8; i += 256) {  // [64 co][64 k] bf16 -> pitch 72
+  for (int i = tid; i < 64 * 8; i += 256) {  // [64 co][64 k] bf16 -> pitch STEM_WPITCH
     const int co = i >> 3, c8 = (i & 7) * 8;
     uint4 wv = *(const uint4*)((const u16*)a.w + co * 64 + c8);
     if (TRAIN && a.bias[co] < 0.f) wv ^= make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);  // y' = -y
-    *(uint4*)(s_w + co * 72 + c8) = wv;
-    if constexpr (X3) *(uint4*)(s_wl + co * 72 + c8) = *(const uint4*)((const u16*)a.w + 64 * 64 + co * 64 + c8);
+    *(uint4*)(s_w + co * STEM_WPITCH + c8) = wv;
+    if constexpr (X3)
+      *(uint4*)(s_wl + co * STEM_WPITCH + c8) = *(const uint4*)((const u16*)a.w + 64 * 64 + co * 64 + c8);
   }
   // band element store: bf16, or the hi/lo pair
   auto put = [&](int i, float v) __attribute__((always_inline)) {
@@ -693,8 +700,8 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        bw[j][s] = *(const uint4*)(s_w + (j * 16 + fr) * 72 + 32 * s + 8 * fg);
-        if constexpr (X3) bwl[j][s] = *(const uint4*)(s_wl + (j * 16 + fr) * 72 + 32 * s + 8 * fg);
+        bw[j][s] = *(const uint4*)(s_w + (j * 16 + fr) * STEM_WPITCH + 32 * s + 8 * fg);
+        if constexpr (X3) bwl[j][s] = *(const uint4*)(s_wl + (j * 16 + fr) * STEM_WPITCH + 32 * s + 8 * fg);
       }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -795,7 +802,8 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
           const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pq, 0xB1, 0xF, 0xF, true);  // quad_perm 1,0,3,2
           const uint32_t w = __builtin_amdgcn_perm(pn, pq, even ? 0x05040100u : 0x03020706u);
           const int q = wave * 32 + i * 8 + 2 * fg + (even ? 0 : 1);
-          *(uint32_t*)(s_out + q * OPITCH + (j * 16 + (fr & ~1)) * 2) = w;
+          const int bo = (j * 16 + (fr & ~1)) * 2;  // byte in the pixel: chunk j * 2 + (fr >> 3)
+          *(uint32_t*)(s_out + q * OPITCH + ((((bo >> 4) ^ stem_oswz(q)) << 4) | (bo & 15))) = w;
           continue;
         }
         const float oa = TRAIN ? fmaxf(fmaxf(left, x[0]), x[1]) : fmaxf(fmaxf(fmaxf(left, x[0]), x[1]) + bias[j], 0.f);
@@ -813,7 +821,9 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
           *(uint32_t*)(s_out + q * OPITCH + pc * 2 + 64) =
               (uint32_t)f2bf(v0 - bf2f(h0)) | ((uint32_t)f2bf(v1 - bf2f(h1)) << 16);
         } else {
-          *(uint32_t*)(s_out + q * OPITCH + c0 * 2) = (uint32_t)h0 | ((uint32_t)h1 << 16);
+          const int bo = c0 * 2;
+          *(uint32_t*)(s_out + q * OPITCH + ((((bo >> 4) ^ stem_oswz(q)) << 4) | (bo & 15))) =
+              (uint32_t)h0 | ((uint32_t)h1 << 16);
         }
       }
     }
@@ -823,7 +833,8 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
 #pragma unroll
     for (int k = 0; k < PXE / 16; ++k) {
       const int idx = (k * 256 + tid) * 8;  // 16 (X3: 32) KB row, 16 B per thread per k
-      *(uint4*)(out + idx) = *(const uint4*)(s_out + (idx / PXE) * OPITCH + (idx % PXE) * 2);
+      const int px = idx / PXE, c = (idx % PXE) / 8;  // pooled pixel, 16-B chunk
+      *(uint4*)(out + idx) = *(const uint4*)(s_out + px * OPITCH + ((X3 ? c : c ^ stem_oswz(px)) << 4));
     }
     __syncthreads();
   }

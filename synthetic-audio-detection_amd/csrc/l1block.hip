@@ -19,16 +19,20 @@
 // barrier: two barriers per tile (intermediate published; intermediate and
 // patch free again).
 //
-// conv1 computes the 18 x 18 intermediate (1-pixel halo for conv2) as 21
-// fragments of 16 pixels: 18 row-aligned ones (row y, columns 0-15) and 3
-// "leftover" ones holding columns 16-17 (pixel (8m + fr/2, 16 + (fr & 1)) of
-// fragment m; the last has 4 live pixels).  Wave pg takes rows 9pg..9pg+8 and
-// leftovers pg and 2+pg (m = 3 is a duplicate of m = 2's row 17: harmless
-// identical writes).  The 1.31x conv1 MFMA work (21 vs 16 fragments) is the
-// price of the fusion; the block runs 1.16x the MFMA work of two plain convs.
+// conv1 computes the 18 x 18 intermediate (1-pixel halo for conv2) in
+// fragments of 16 pixels: row-aligned ones (row y, columns 0-15) and
+// "leftover" ones holding columns 16-17 (pixel (y0 + fr/2, 16 + (fr & 1))).
+// A workgroup walks its tiles down column strips (ty fastest), so a tile that
+// continues a strip takes intermediate rows 0, 1 and patch rows 2, 3 from the
+// tile above (LDS-to-LDS copies of its rows 16, 17 and 18, 19) and computes
+// rows 2-17 only: wave pg takes rows 2+8pg .. 9+8pg (8 aligned + 1 leftover
+// fragment), 18 fragments per tile (16 without the halo), and its patch needs
+// 40 DMA pieces instead of 50.  The first tile of a strip also computes rows
+// 0, 1 (3 more fragments).  At 8 tiles per strip (128 x 128 maps) conv1 runs
+// 1.15x its halo-free MFMA work (21 fragments: 1.31x).
 //
-// LDS (144 KB): 2 x input patch [20 x 20 pixels][128 B] (the next tile's patch
-// is DMA'd during this tile's conv1, one piece per K-step), the intermediate
+// LDS (142 KB): 2 x input patch [20 x 20 pixels][128 B] (the next tile's patch
+// is DMA'd during this tile's conv1, one piece per 5 units), the intermediate
 // [18 rows][18 x 128 B + 16 B pad] and the biases.  Swizzles (16-B chunk c of a
 // pixel):
 //  * intermediate pixel (y, x): position c ^ key(x) -- a column key that is
@@ -74,8 +78,10 @@ constexpr int OFF_B = OFF_I + IWD * IROW;  // b1 [64], b2 [64] fp32
 constexpr int SMEM = OFF_B + 2 * 64 * 4;
 constexpr int NDP = PR / 8;                // 50 DMA pieces of 8 pixel rows
 constexpr int QP = (NDP + NW - 1) / NW;    // 13 per wave (waves 2, 3: 12)
-constexpr int NA = 9;                      // row-aligned conv1 fragments per wave
-constexpr int NF = NA + 2;                 // + 2 leftover fragments
+constexpr int NA = 8;                      // row-aligned conv1 fragments per wave (rows 2 + 8 pg + k)
+constexpr int NF = NA + 1;                 // + 1 leftover fragment (columns 16, 17 of those rows)
+constexpr int QSKIP = 10;                  // pieces 0-9 = patch rows 0-3: a continuation tile needs no
+                                           // rows 0, 1 and copies rows 2, 3 from the previous patch
 constexpr int NS = 18;                     // K-steps per conv: 9 taps x 2 halves of 32 channels
 constexpr int NU1 = NS * NF;               // conv1 (read, 2 MFMA) units per wave
 constexpr int NU2 = NS * 8;                // conv2 units per wave
@@ -107,7 +113,7 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
   const int cg = wave & 1, pg = wave >> 1;
   const int cw = cg * 32;  // this wave's first channel (both convs)
   const int w = xcd_remap(blockIdx.x, gridDim.x);
-  const int tiles_x = a.W / 16, tiles_img = tiles_x * (a.H / 16);
+  const int tiles_y = a.H / 16, tiles_img = (a.W / 16) * tiles_y;
   const int tiles_p = a.N * tiles_img;
   const int tp_begin = (int)((int64_t)w * tiles_p / gridDim.x), tp_end = (int)((int64_t)(w + 1) * tiles_p / gridDim.x);
   if (tp_begin >= tp_end) return;  // whole workgroup (uniform)
@@ -134,19 +140,21 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
   struct TileO {
     int base, oy0, ox0;
   };
+  // tiles run down column strips (ty fastest), so a tile's top halo is the
+  // previous tile's bottom rows
   auto tile_o = [&](int t) __attribute__((always_inline)) {
     const int b = t / tiles_img, rem = t - b * tiles_img;
-    const int ty = rem / tiles_x;
+    const int tx = rem / tiles_y;
     TileO o;
-    o.oy0 = ty * 16;
-    o.ox0 = (rem - ty * tiles_x) * 16;
+    o.oy0 = (rem - tx * tiles_y) * 16;
+    o.ox0 = tx * 16;
     o.base = ((b * a.H + o.oy0) * a.W + o.ox0) * 128;
     return o;
   };
   // (branch-free: the bounds test is VALU in the MFMA shadow; only the piece
   // count per wave is a uniform branch)
-  auto issue_piece = [&](int k, const TileO& o, int buf) __attribute__((always_inline)) {
-    if (wave + NW * k >= NDP) return;  // uniform
+  auto issue_piece = [&](int k, const TileO& o, int buf, bool cont) __attribute__((always_inline)) {
+    if (wave + NW * k >= NDP || (cont && wave + NW * k < QSKIP)) return;  // uniform
     const int Y = DYX[k] & 0xFFFF, X = DYX[k] >> 16;
     const bool ok = (unsigned)(o.oy0 - 2 + Y) < (unsigned)a.H && (unsigned)(o.ox0 - 2 + X) < (unsigned)a.W;
     dma16_m0(rx, ok ? o.base + DREL[k] : BAD, lds0 + buf * PATCH + (wave + NW * k) * 1024);
@@ -170,7 +178,7 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
     *(float4*)(smem + OFF_B + 16 * tid) = *(const float4*)src;
   }
 #pragma unroll
-  for (int k = 0; k < QP; ++k) issue_piece(k, tile_o(tp_begin), 0);
+  for (int k = 0; k < QP; ++k) issue_piece(k, tile_o(tp_begin), 0, false);
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -200,10 +208,16 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
     // free buffer, which nothing reads -- no branch around the DMA)
     const TileO onext = tile_o(has_next ? t + 1 : t);
     const int b = t / tiles_img, rem = t - b * tiles_img;
-    const int ty = rem / tiles_x;
-    const int oy0 = ty * 16, ox0 = (rem - ty * tiles_x) * 16;
+    const int tx = rem / tiles_y, ty = rem - tx * tiles_y;
+    const int oy0 = ty * 16, ox0 = tx * 16;
+    // continuation tile (uniform): the previous tile is the one above it, so
+    // intermediate rows 0, 1 and patch rows 2, 3 are copies of its rows 16, 17
+    // and 18, 19 (LDS to LDS), and conv1 computes rows 2-17 only: 18 fragments
+    // instead of 21, 40 patch pieces instead of 50
+    const bool cont = t > tp_begin && ty > 0;
+    const bool next_cont = has_next && onext.oy0 > 0;
     const int pbo = pb * PATCH;
-    const int pboa = pbo + pg * 9 * PROW;  // aligned fragments: rows 9pg + k
+    const int pboa = pbo + (2 + 8 * pg) * PROW;  // aligned fragments: rows 2 + 8pg + k
     // Lane constants, derived per tile from an opaque copy of the lane id:
     // the fragment addresses are tile-invariant, and hoisted out of the tile
     // loop they would take registers next to the 288 of resident weights.
@@ -211,30 +225,22 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
     asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
     const int frt = ln & 15, fgt = ln >> 4, et = ln & 1;
     // aligned fragment, patch column frt + kx: pixel row + chunk position of channel group fgt
-    int LAt[3], KXt[3], LYt[2], LR0t[2];
+    int LAt[3], KXt[3];
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
       LAt[kx] = (frt + kx) * 128 + ((fgt ^ l1b_key(frt + kx)) << 4);
       KXt[kx] = fgt ^ l1b_key(16 + et + kx);
     }
-    // leftover fragments l = 0, 1 (m = pg, 2 + pg): pixel (LYt, 16 + et)
-#pragma unroll
-    for (int l = 0; l < 2; ++l) {
-      const int m = l == 0 ? pg : 2 + pg;
-      LYt[l] = min(8 * m + (frt >> 1), IWD - 1);
-      LR0t[l] = (LYt[l] * PWD + 16 + et) * 128;
-    }
+    // the leftover fragment: pixel (LYt, 16 + et), rows 2 + 8pg .. 9 + 8pg
+    const int LYt = 2 + 8 * pg + (frt >> 1);
     // per-tile read bases: aligned (+ the patch buffer and the wave's row
     // block), leftover (+ buffer) and the leftover row terms per tap row
-    int LAp[3], LRb[2], LYG[2][3];
+    int LAp[3], LYG[3];
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) LAp[kx] = LAt[kx] + pboa;
+    const int LRb = (LYt * PWD + 16 + et) * 128 + pbo;
 #pragma unroll
-    for (int l = 0; l < 2; ++l) {
-      LRb[l] = LR0t[l] + pbo;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) LYG[l][ky] = ((LYt[l] + ky) & 3) << 1;
-    }
+    for (int ky = 0; ky < 3; ++ky) LYG[ky] = ((LYt + ky) & 3) << 1;
 
     // ---------------- conv1: 18 x 18 intermediate ----------------
     // Unit = one fragment read + its two MFMAs (channel tiles i = 0, 1).
@@ -250,14 +256,13 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
       constexpr int s = l1b_s1(u), k = l1b_k1(u);
       constexpr int tap = s >> 1, h = s & 1, ky = tap / 3, kx = tap % 3;
       if constexpr (k < NA) {
-        const int Y = 9 * pg + k + ky;                       // uniform
-        const int sg = ((Y & 3) << 5) ^ (h << 6);            // 2 (Y & 3) and the K-half, as chunk bits
+        // patch row Y = 2 + 8pg + k + ky: Y & 3 is a constant
+        constexpr int sg = (((2 + k + ky) & 3) << 5) ^ (h << 6);  // 2 (Y & 3) and the K-half, as chunk bits
         // (pboa is a multiple of 128, so it commutes with the XOR on bits 4-6)
         return *(const uint4*)(smem + (LAp[kx] ^ sg) + (k + ky) * PROW);
       } else {
-        constexpr int l = k - NA;
-        const int pos = KXt[kx] ^ LYG[l][ky] ^ (h << 2);
-        return *(const uint4*)(smem + (LRb[l] + (pos << 4)) + (ky * PWD + kx) * 128);
+        const int pos = KXt[kx] ^ LYG[ky] ^ (h << 2);
+        return *(const uint4*)(smem + (LRb + (pos << 4)) + (ky * PWD + kx) * 128);
       }
     };
     f32x4 b1v[2];
@@ -277,11 +282,11 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
       if constexpr (part == 0) {
         int y, x;
         if constexpr (k < NA) {
-          y = 9 * pg + k;
+          y = 2 + 8 * pg + k;
           x = frt;
           e1_inm = (unsigned)(oy0 - 1 + y) < (unsigned)a.H ? cma : 0u;  // row test uniform
         } else {
-          y = LYt[k - NA];
+          y = LYt;
           x = 16 + et;
           e1_inm = (unsigned)(oy0 - 1 + y) < (unsigned)a.H ? cml : 0u;
         }
@@ -302,6 +307,66 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
         *(uint2*)(smem + (i ? e1_addr1 : e1_addr)) = q;
       }
     };
+    if (cont) {
+      // intermediate rows 16, 17 of the tile above -> rows 0, 1: each pg = 1
+      // wave copies its own channel half (those waves write rows 16, 17 later
+      // in this conv1, and one wave's LDS operations complete in order)
+      if (pg == 1) {
+        // 144 16-B chunks (2 rows x 18 pixels x 4 chunks), 3 per lane
+        auto off = [&](int r) __attribute__((always_inline)) {
+          const int i = min(ln + 64 * r, 143), row = i >= 72, rem = i - 72 * row, x = rem >> 2;
+          return row * IROW + x * 128 + ((((cw >> 3) + (rem & 3)) ^ l1b_key(x)) << 4);
+        };
+        const int o0 = off(0), o1 = off(1), o2 = off(2);
+        const uint4 v0 = *(const uint4*)(smem + OFF_I + 16 * IROW + o0);
+        const uint4 v1 = *(const uint4*)(smem + OFF_I + 16 * IROW + o1);
+        const uint4 v2 = *(const uint4*)(smem + OFF_I + 16 * IROW + o2);
+        *(uint4*)(smem + OFF_I + o0) = v0;
+        *(uint4*)(smem + OFF_I + o1) = v1;
+        *(uint4*)(smem + OFF_I + o2) = v2;
+      }
+    } else {
+      // first tile of a strip (or of this workgroup's range): intermediate
+      // rows 0, 1 as extra fragments -- wave pg computes row pg (columns
+      // 0-15), the pg = 0 waves also columns 16, 17 of both rows (lane frt:
+      // pixel ((frt >> 1) & 1, 16 + et); lanes 4-15 duplicate lanes 0-3)
+      auto prefix = [&](bool left) __attribute__((always_inline)) {
+        const int y = left ? (frt >> 1) & 1 : pg;
+        f32x4 pa[2];
+#pragma unroll
+        for (int st = 0; st < NS; ++st) {
+          const int tap = st >> 1, h = st & 1, ky = tap / 3, kx = tap % 3;
+          const int Y = y + ky;
+          const int ad = left ? pbo + (Y * PWD + 16 + et + kx) * 128 +
+                                    ((KXt[kx] ^ ((Y & 3) << 1) ^ (h << 2)) << 4)
+                              : pbo + (LAt[kx] ^ (((Y & 3) << 5) ^ (h << 6))) + Y * PROW;
+          const uint4 bf = *(const uint4*)(smem + ad);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            if (st == 0)
+              l1b_mfma_ac(pa[i], w1r[i][st], bf, b1v[i]);
+            else
+              l1b_mfma_a(pa[i], w1r[i][st], bf);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 11" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const int x = left ? 16 + et : frt;
+        const uint32_t inm = (unsigned)(oy0 - 1 + y) < (unsigned)a.H ? (left ? cml : cma) : 0u;
+        const int pix = OFF_I + y * IROW + x * 128;
+        const int pos = (((cw >> 3) + (fgt >> 1)) ^ l1b_key(x)) * 16 + (fgt & 1) * 8;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          uint2 q;
+          q.x = l1b_relu2(l1b_pk(pa[i][0], pa[i][1])) & inm;
+          q.y = l1b_relu2(l1b_pk(pa[i][2], pa[i][3])) & inm;
+          *(uint2*)(smem + pix + (i ? pos ^ 32 : pos)) = q;
+        }
+      };
+      prefix(false);
+      if (pg == 0) prefix(true);
+    }
     uint4 bq[DQ];
     l1b_for<DQ>([&](auto uc) __attribute__((always_inline)) { bq[decltype(uc)::value] = rd1(uc); });
     l1b_for<NU1>([&](auto uc) __attribute__((always_inline)) {
@@ -310,7 +375,7 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
       const uint4 bf = bq[u % DQ];
       if constexpr (u + DQ < NU1) bq[u % DQ] = rd1(std::integral_constant<int, u + DQ>{});
       if constexpr (u % 5 == 0 && u / 5 < QP)
-        issue_piece(u / 5, onext, pb ^ 1);
+        issue_piece(u / 5, onext, pb ^ 1, next_cont);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         if constexpr (s == 0)
@@ -401,12 +466,27 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
                                               (jj * a.W + fr2) * 128 + (cw + 16 * i + 4 * fg2) * 2, obase, 0);
       }
     };
+    // the next tile continues this strip: its patch rows 2, 3 are this patch's
+    // rows 18, 19 (same swizzle: Y & 3 and X agree), copied now -- buffer
+    // pb ^ 1 is free and its DMA pieces cover rows 4-19 only; 320 16-B chunks
+    const int pci1 = min(tid + 256, 319);
+    uint4 pcv0 = {0, 0, 0, 0}, pcv1 = {0, 0, 0, 0};
+    if (next_cont) {
+      pcv0 = *(const uint4*)(smem + pbo + 360 * 128 + tid * 16);
+      pcv1 = *(const uint4*)(smem + pbo + 360 * 128 + pci1 * 16);
+    }
     l1b_for<DQ>([&](auto uc) __attribute__((always_inline)) { bq[decltype(uc)::value] = rd2(uc); });
     l1b_for<NU2>([&](auto uc) __attribute__((always_inline)) {
       constexpr int u = decltype(uc)::value;
       constexpr int s = u % NS, jj = u / NS;
       const uint4 bf = bq[u % DQ];
       if constexpr (u + DQ < NU2) bq[u % DQ] = rd2(std::integral_constant<int, u + DQ>{});
+      if constexpr (u == 3) {
+        if (next_cont) {
+          *(uint4*)(smem + (pb ^ 1) * PATCH + 40 * 128 + tid * 16) = pcv0;
+          *(uint4*)(smem + (pb ^ 1) * PATCH + 40 * 128 + pci1 * 16) = pcv1;
+        }
+      }
       l1b_for<2>([&](auto ic) __attribute__((always_inline)) {
         constexpr int i = decltype(ic)::value;
         // the last K-steps' weights of channel tile 1 sit in VGPRs

@@ -14,6 +14,12 @@ still identical).  bf16 is reported with the bar of the bf16 noise it carries
 resnet34, 0.5 for resnet50 (measured 0.245 merged / 0.398 per head with the
 layer3/4 3x3 convs on variant 31, 0.26 / <= 0.25 on variant 13: the two sum K
 in different orders, and 16 Bottlenecks amplify the bf16 rounding flips).
+The 0.5 is the bf16 ARITHMETIC's, not a kernel's: tools/deep_bf16_budget.py
+emulates the bf16 plan on the CPU (no device kernel involved) under 8 fp32
+summation orders and gets 0.29 .. 0.43 per head and 0.21 .. 0.24 merged
+against the same fixture (profiles/r04_resnet50_bf16_order_spread.txt), so
+variant 31's 0.398 is inside the spread of orders and variant 13's 0.25 at its
+low end.
 """
 import os
 

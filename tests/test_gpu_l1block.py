@@ -65,7 +65,11 @@ def _torch_ref(x, w1, b1, w2, b2):
     return y.permute(0, 2, 3, 1)
 
 
-@pytest.mark.parametrize('N,H,W', [(1, 16, 16), (2, 48, 32), (3, 128, 128), (5, 64, 80), (37, 128, 128)])
+# (round 4: tiles run down column strips and a tile that continues one copies
+# its top halo from the tile above; 37 x 128^2, 40 x 64 x 48 and 300 x 48 x 16
+# give workgroups several tiles with ranges that start and end mid-strip)
+@pytest.mark.parametrize('N,H,W', [(1, 16, 16), (2, 48, 32), (3, 128, 128), (5, 64, 80), (37, 128, 128),
+                                   (40, 64, 48), (300, 48, 16)])
 def test_fused_block_matches_unfused(N, H, W):
     ops = _operands(N, H, W, N * 1000 + H + W)
     out = _fused(*ops)

@@ -1,10 +1,13 @@
 """CPU: the fused layer1 BasicBlock kernel's LDS layouts (csrc/l1block.hip,
 variant 40), checked exhaustively with the kernel's own index formulas.
 
-* conv1's 21 fragments per tile (18 row-aligned + 3 leftover column-16/17
-  fragments, split over the two pixel-group waves) cover every pixel of the
-  18 x 18 intermediate, and every lane that does not own a live pixel
-  duplicates one that does (its writes are then identical);
+* conv1's fragments cover every pixel of the 18 x 18 intermediate: a tile
+  that continues a column strip (round 4) computes rows 2-17 as 16 row-aligned
+  + 2 leftover column-16/17 fragments, one of each kind per pixel-group wave
+  (rows 0, 1 are the tile above's rows 16, 17, copied in LDS); the first tile
+  of a strip adds the prefix fragments of rows 0, 1 (row pg, and columns
+  16, 17 of both rows on the pg = 0 waves); every lane that does not own a
+  live pixel duplicates one that does (its writes are then identical);
 * every ds_read_b128 fragment read (conv1 from the 20 x 20 input patch, conv2
   from the intermediate) is free of LDS bank conflicts under the MI355X
   ds_read_b128 lane grouping (MI355X_MICROARCH.md, LDS table: 4 groups of 16
@@ -45,45 +48,63 @@ def lds_cycles(addrs):
     return tot
 
 
+# conv1 fragments of a wave: k = 0..7 aligned rows 2 + 8pg + k, k = 8 the
+# leftover (rows 2 + 8pg .. 9 + 8pg, columns 16, 17); first tiles of a strip
+# add 'PA' (aligned row pg) and, on pg = 0 waves, 'PL' (columns 16, 17 of rows 0, 1)
+FRAGS = list(range(9)) + ['PA', 'PL']
+
+
 def conv1_fragment(pg, k, ln):
     """intermediate pixel (y, x) of lane ln in conv1 fragment k of pixel group pg"""
     fr = ln & 15
-    if k < 9:
-        return 9 * pg + k, fr
-    m = pg if k == 9 else 2 + pg
-    return min(8 * m + (fr >> 1), IWD - 1), 16 + (fr & 1)
+    if k == 'PA':
+        return pg, fr
+    if k == 'PL':
+        return (fr >> 1) & 1, 16 + (fr & 1)
+    if k < 8:
+        return 2 + 8 * pg + k, fr
+    return 2 + 8 * pg + (fr >> 1), 16 + (fr & 1)
 
 
 def conv1_addr(pg, k, ln, ky, kx, h):
-    """the kernel's rd1 address (patch buffer 0)"""
+    """the kernel's read address (patch buffer 0): rd1 for the strip fragments,
+    the prefix lambda's for PA / PL"""
     fr, fg = ln & 15, ln >> 4
-    if k < 9:
-        Y = 9 * pg + k + ky
-        LA = (fr + kx) * 128 + ((fg ^ key(fr + kx)) << 4)
-        sg = ((Y & 3) << 5) ^ (h << 6)
-        return (LA ^ sg) + pg * 9 * PROW + (k + ky) * PROW
-    l = k - 9
-    m = pg if l == 0 else 2 + pg
     e = fr & 1
-    LY = min(8 * m + (fr >> 1), IWD - 1)
-    LR0 = (LY * PWD + 16 + e) * 128
+    LA = (fr + kx) * 128 + ((fg ^ key(fr + kx)) << 4)
     KX = fg ^ key(16 + e + kx)
+    if k == 'PA':
+        Y = pg + ky
+        return (LA ^ (((Y & 3) << 5) ^ (h << 6))) + Y * PROW
+    if k == 'PL':
+        Y = ((fr >> 1) & 1) + ky
+        return (Y * PWD + 16 + e + kx) * 128 + ((KX ^ ((Y & 3) << 1) ^ (h << 2)) << 4)
+    if k < 8:
+        sg = (((2 + k + ky) & 3) << 5) ^ (h << 6)
+        return ((LA + (2 + 8 * pg) * PROW) ^ sg) + (k + ky) * PROW
+    LY = 2 + 8 * pg + (fr >> 1)
+    LRb = (LY * PWD + 16 + e) * 128
     pos = KX ^ (((LY + ky) & 3) << 1) ^ (h << 2)
-    return LR0 + (pos << 4) + (ky * PWD + kx) * 128
+    return LRb + (pos << 4) + (ky * PWD + kx) * 128
+
+
+def frags_of(pg):
+    return [k for k in FRAGS if not (k == 'PL' and pg == 1)]
 
 
 def test_conv1_fragments_cover_the_intermediate():
-    live = set()
+    strip, first = set(), set()
     for pg in range(2):
-        for k in range(11):
+        for k in frags_of(pg):
             for ln in range(16):
-                live.add(conv1_fragment(pg, k, ln))
-    assert live == {(y, x) for y in range(IWD) for x in range(IWD)}
+                (first if k in ('PA', 'PL') else strip).add(conv1_fragment(pg, k, ln))
+    assert strip == {(y, x) for y in range(2, IWD) for x in range(IWD)}
+    assert first == {(y, x) for y in range(2) for x in range(IWD)}
 
 
 def test_conv1_reads_are_conflict_free_and_hit_the_right_chunk():
     for pg in range(2):
-        for k in range(11):
+        for k in frags_of(pg):
             for ky in range(3):
                 for kx in range(3):
                     for h in range(2):
@@ -164,7 +185,7 @@ def test_conv1_intermediate_stores_at_most_2_way():
     for pg in range(2):
         for cg in range(2):
             cw = 32 * cg
-            for k in range(11):
+            for k in frags_of(pg):
                 for i in range(2):
                     addrs = []
                     for ln in range(64):
@@ -177,3 +198,16 @@ def test_conv1_intermediate_stores_at_most_2_way():
                         addrs.append(a)
                     worst = max(worst, write_b64_cycles(addrs))
     assert worst <= 8, worst  # 4 groups x 2-way
+
+
+def test_strip_copies_keep_the_swizzle():
+    """a continuation tile's LDS copies: patch rows 18, 19 -> 2, 3 byte for byte
+    (same Y & 3 and X, so every chunk lands where the readers expect it), and
+    intermediate rows 16, 17 -> 0, 1 per pixel chunk (the key depends on x only)"""
+    for X in range(PWD):
+        for c in range(8):
+            for dy in range(2):
+                assert patch_pos(18 + dy, X, c) == patch_pos(2 + dy, X, c)
+                assert (360 + 20 * dy + X) * 128 - 360 * 128 == (40 + 20 * dy + X) * 128 - 40 * 128
+    # pieces 0..9 hold exactly patch rows 0..3 (slots 0..79)
+    assert all(8 * q + 7 < 80 for q in range(10)) and 8 * 10 == 80

@@ -1,12 +1,13 @@
 #!/bin/bash
 # Same-box bench runs of labelled (lib, env) configurations, interleaved:
 #   bash tools/ab_env.sh "base:SAD_FRONT_MB=0 tree:SAD_FRONT_MB=32" [rounds]
+# (BENCH_ARGS="--dtype bf16x3" times the parity mode instead)
 N=${2:-2}
 for i in $(seq $N); do
   for cfg in $1; do
     lib=${cfg%%:*}; envs=${cfg#*:}; [ "$envs" = "$cfg" ] && envs=""
     L=synthetic-audio-detection_amd/sad/libsad.so; [ "$lib" != tree ] && L=abl/libsad_$lib.so
-    r=$(env SAD_LIB=$L ${envs//,/ } timeout -k 10 120 python bench.py --kernels-only --steps 20 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], r["launch_avg_us"], r["backbone"]["ms_per_step"], r.get("frontend", {}).get("ms_per_step"))') || exit 1
+    r=$(env SAD_LIB=$L ${envs//,/ } timeout -k 10 120 python bench.py --kernels-only --steps 20 $BENCH_ARGS | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], r["launch_avg_us"], r["backbone"]["ms_per_step"], r.get("frontend", {}).get("ms_per_step"))') || exit 1
     echo "$cfg: $r"
   done
 done
