@@ -699,7 +699,7 @@ int launch_halo256(const BlockConvArgs& a, hipStream_t s, bool x3);
 int launch_halo256r(const BlockConvArgs& a, hipStream_t s, bool x3);
 bool halo256_ok(const BlockConvArgs& a);
 int launch_halo_rw(const BlockConvArgs& a, hipStream_t s);
-int launch_l2conv(const BlockConvArgs& a, hipStream_t s);
+int launch_l2conv(const BlockConvArgs& a, hipStream_t s, bool x3 = false);
 int launch_halo256s2(const BlockConvArgs& a, hipStream_t s);
 bool halo256s2_ok(const BlockConvArgs& a);
 int launch_halo_rw_x3(const BlockConvArgs& a, hipStream_t s);
@@ -816,6 +816,17 @@ static int halo_c128_variant() {
   }();
   return v;
 }
+// SAD_X3_L1 (split-bf16 layer1, A/B): 42 = the resident-weight conv of layer2's
+// bf16 kernel in its split form (l2conv.hip: 288 weight registers per wave, all
+// 64 logical channels per workgroup, 3 MFMAs per fragment read), 26 = round 2's
+// half-the-channels kernel (weights in LDS)
+static int x3_l1_variant() {
+  static const int v = [] {
+    const char* e = getenv("SAD_X3_L1");
+    return e ? atoi(e) : 42;
+  }();
+  return v;
+}
 // SAD_X3_RW=0 runs split-bf16 layer1 on the weight-ring halo kernel (variant 20) instead of variant 26 (A/B)
 static bool x3_rw() {
   static const bool v = [] {
@@ -852,6 +863,7 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   // layer2 (Cout 128), whose implicit GEMM is L2->LDS-fill bound
   if (dtype == SAD_BF16X3) {
     // layer1 (64 -> 64): the resident-weight split-bf16 kernel (half the channels per workgroup)
+    if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64 && x3_l1_variant() == 42) return 42;
     if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64 && x3_rw()) return 26;
     if (x3_layer2_v31() && a.Cout == 128 && halo31_ok(a)) return 31;
     if (halo256_mode() == 1 && halo256_ok(a)) return 30;
@@ -907,7 +919,7 @@ bool block_conv_can_pool(const BlockConvArgs& a, int dtype) {
   return bp > 0 && a.Ho * a.Wo == bp && !a.res && a.M % bp == 0 && (v != 31 || a.Cout % 256 == 0);
 }
 static bool variant_fits(int v, int cout) {
-  if (v == 26) return cout == 64;
+  if (v == 26 || v == 42) return cout == 64;
   if (v == 30) return cout % 256 == 0;
   if (v == 31 || v == 32) return cout % 128 == 0;
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128, 128};
@@ -1079,6 +1091,11 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   if (v == 41) {
     SAD_REQUIRE(dtype == SAD_BF16 && (halo_ok(a_in, dtype) || l2conv_ds_ok(a_in)), "variant 41: bf16 3x3/s1/p1, H, W % 16");
     return launch_l2conv(a, s);
+  }
+  if (v == 42) {
+    SAD_REQUIRE(dtype == SAD_BF16X3 && halo_ok(a_in, dtype) && a_in.Cin == 64 && a_in.Cout == 64,
+                "variant 42: split-bf16 64 -> 64 3x3/s1/p1, H, W % 16");
+    return launch_l2conv(a, s, true);
   }
   if (dtype == SAD_BF16X3 && v == 26) {
     SAD_REQUIRE(halo_ok(a_in, dtype), "split-bf16 halo conv: 3x3/s1/p1, H, W % 16");

@@ -29,6 +29,16 @@
 // the 64 K columns behind the taps, 16 more VGPRs per wave), over a 16 x 16
 // pixel patch of the input at stride 2 DMA'd to LDS during chunk 0 (16-B chunk
 // c of pixel p at c ^ ((p >> 1) & 7): conflict-free fragment reads).
+//
+// X3 (variant 42, round 4): the split-bf16 parity mode's layer1 convs, logical
+// Cin = Cout = 64 = 128 bf16 input channels ([hi 32 | lo 32] x 2 chunks, the
+// same 2 x 128-B chunks per pixel as the bf16 128-channel conv): the same 288
+// resident weight registers per wave then hold 32 logical output channels'
+// hi and lo weights, so the 4 waves are 2 channel groups x 2 pixel halves (8
+// fragments each).  Per fragment and tap the hi fragment feeds W_hi.X_hi and
+// W_lo.X_hi, the lo fragment W_hi.X_lo: 3 MFMAs per fragment read (bf16: 2).
+// The identity residual (hi + lo, 256 B per pixel) has the 128-channel conv's
+// LDS tile layout; the epilogue splits relu(acc + res) into hi / lo again.
 #include "common.hpp"
 #include "igemm.hpp"
 #include "kernels.hpp"
@@ -50,7 +60,6 @@ constexpr int OFF_RES = 2 * PATCH;
 constexpr int SMEM_RES = OFF_RES + RESB;
 constexpr int NS = 36;                         // K-steps: 2 chunks x 9 taps x 2 halves of 32 channels
 constexpr int NSC = 18;                        // per chunk
-constexpr int NU = NSC * 16;                   // (read, 2 MFMA) units per chunk
 constexpr int DQ = 4;                          // fragment reads in flight
 constexpr int WV = 8;                          // K-steps of channel tile 1 whose weights sit in VGPRs
 constexpr int BAD = 0x7FFFFFF0;
@@ -60,15 +69,21 @@ static_assert(SMEM_RES + 512 <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ int l2c_key(int x) { return (int)((l2c::KEY >> (3 * x)) & 7); }
 
-template <bool RES, bool DS>
+template <bool RES, bool DS, bool X3 = false>
 __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
-  static_assert(!(RES && DS), "one shortcut form");
+  static_assert(!(RES && DS) && !(X3 && DS), "one shortcut form");
   using namespace l2c;
+  constexpr int TP = X3 ? 8 : 16;       // fragments (tile rows) per wave
+  constexpr int UPT = 2 * TP;           // units per tap: (fragment, K-half)
+  constexpr int NUC = 9 * UPT;          // units per chunk
+  constexpr int PDIV = X3 ? 8 : 16;     // units between patch DMA pieces
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
-  const int cw = wave * 32;  // this wave's first output channel
+  // this wave's first output channel (logical) and first tile row
+  const int cw = X3 ? (wave & 1) * 32 : wave * 32;
+  const int r0w = X3 ? (wave >> 1) * 8 : 0;
   const int w = xcd_remap(blockIdx.x, gridDim.x);
   const int tiles_x = a.W / 16, tiles_img = tiles_x * (a.H / 16);
   const int tiles_p = a.N * tiles_img;
@@ -160,7 +175,8 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
                                   (fg + 4 * h) * 8);
     }
   // the bias (the accumulators' start value) behind the LDS buffers
-  if (tid < 32) *(float4*)(smem + (RES || DS ? SMEM_RES : OFF_RES) + 16 * tid) = *(const float4*)(a.bias + 4 * tid);
+  if (tid < (X3 ? 16 : 32))
+    *(float4*)(smem + (RES || DS ? SMEM_RES : OFF_RES) + 16 * tid) = *(const float4*)(a.bias + 4 * tid);
   auto biasv = [&](int i) __attribute__((always_inline)) {
     return *(const f32x4*)(smem + (RES || DS ? SMEM_RES : OFF_RES) + (cw + 16 * i + fg * 4) * 4);
   };
@@ -175,12 +191,12 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
   // flight); the bias is visible after it
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  f32x4 acc[2][16];
+  f32x4 acc[2][TP];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const f32x4 b0 = biasv(i);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[i][j] = b0;
+    for (int j = 0; j < TP; ++j) acc[i][j] = b0;
   }
 
   for (int t = tp_begin; t < tp_end; ++t) {
@@ -213,31 +229,49 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
       for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
         for (int h = 0; h < 2; ++h) I2c[kx][h] = I2[kx][h] + c * PATCH;
+      // unit u of the chunk: tap u / UPT; bf16: K-half h = (u % UPT) / 16,
+      // fragment j = u % 16 (K-half-outer, as round 3); X3: fragment
+      // j = (u % UPT) / 2, h = u % 2 (the hi fragment, then the lo one)
       auto rd = [&](auto uc) __attribute__((always_inline)) -> uint4 {
         constexpr int u = decltype(uc)::value;
-        constexpr int sl = u / 16, j = u % 16;
-        constexpr int tap = sl >> 1, h = sl & 1, ky = tap / 3, kx = tap % 3;
-        return *(const uint4*)(smem + I2c[kx][h] + (j + ky) * ROWB);
+        constexpr int tap = u / UPT, ky = tap / 3, kx = tap % 3;
+        constexpr int j = X3 ? (u % UPT) / 2 : u % 16, h = X3 ? u % 2 : (u % UPT) / 16;
+        return *(const uint4*)(smem + I2c[kx][h] + (r0w + j + ky) * ROWB);
       };
       uint4 bq[DQ];
       l1b_for<DQ>([&](auto uc) __attribute__((always_inline)) { bq[decltype(uc)::value] = rd(uc); });
-      l1b_for<NU>([&](auto uc) __attribute__((always_inline)) {
+      l1b_for<NUC>([&](auto uc) __attribute__((always_inline)) {
         constexpr int u = decltype(uc)::value;
-        constexpr int sl = u / 16, j = u % 16, s = c * NSC + sl;
+        constexpr int tap = u / UPT;
+        constexpr int j = X3 ? (u % UPT) / 2 : u % 16, h = X3 ? u % 2 : (u % UPT) / 16;
+        constexpr int s = c * NSC + 2 * tap + h;   // this fragment's K-step (bf16; X3: its hi / lo weights)
+        constexpr int s_hi = c * NSC + 2 * tap, s_lo = s_hi + 1;
         const uint4 bf = bq[u % DQ];
-        if constexpr (u + DQ < NU) bq[u % DQ] = rd(std::integral_constant<int, u + DQ>{});
-        // DMA: chunk 0 carries this tile's chunk-1 patch (units 0, 16, ...)
-        // and residual (units 8, 24, ...); chunk 1 the next tile's chunk-0 patch
-        if constexpr (u % 16 == 0 && u / 16 < QP) issue_piece(u / 16, c == 0 ? o : onext, c ^ 1);
-        if constexpr (RES && c == 0 && u % 16 == 8 && u / 16 < NRP) issue_res(u / 16, o);
+        if constexpr (u + DQ < NUC) bq[u % DQ] = rd(std::integral_constant<int, u + DQ>{});
+        // DMA: chunk 0 carries this tile's chunk-1 patch and residual; chunk 1
+        // the next tile's chunk-0 patch
+        if constexpr (u % PDIV == 0 && u / PDIV < QP) issue_piece(u / PDIV, c == 0 ? o : onext, c ^ 1);
+        if constexpr (RES && c == 0 && u % PDIV == PDIV / 2 && u / PDIV < NRP) issue_res(u / PDIV, o);
         if constexpr (DS && c == 0 && u % 32 == 8 && u / 32 < NDS) issue_ds(u / 32, o);
-        l1b_for<2>([&](auto ic) __attribute__((always_inline)) {
-          constexpr int i = decltype(ic)::value;
-          if constexpr (i == 1 && s >= NS - WV)
-            l1b_mfma_v(acc[i][j], wr[i][s], bf);
+        auto mm = [&](auto ic, auto sc) __attribute__((always_inline)) {
+          constexpr int i = decltype(ic)::value, ss = decltype(sc)::value;
+          if constexpr (i == 1 && ss >= NS - WV)
+            l1b_mfma_v(acc[i][j], wr[i][ss], bf);
           else
-            l1b_mfma_a(acc[i][j], wr[i][s], bf);
-        });
+            l1b_mfma_a(acc[i][j], wr[i][ss], bf);
+        };
+        if constexpr (!X3) {
+          mm(std::integral_constant<int, 0>{}, std::integral_constant<int, s>{});
+          mm(std::integral_constant<int, 1>{}, std::integral_constant<int, s>{});
+        } else if constexpr (h == 0) {  // the hi fragment: W_hi.X_hi, W_lo.X_hi
+          mm(std::integral_constant<int, 0>{}, std::integral_constant<int, s_hi>{});
+          mm(std::integral_constant<int, 1>{}, std::integral_constant<int, s_hi>{});
+          mm(std::integral_constant<int, 0>{}, std::integral_constant<int, s_lo>{});
+          mm(std::integral_constant<int, 1>{}, std::integral_constant<int, s_lo>{});
+        } else {  // the lo fragment: W_hi.X_lo
+          mm(std::integral_constant<int, 0>{}, std::integral_constant<int, s_hi>{});
+          mm(std::integral_constant<int, 1>{}, std::integral_constant<int, s_hi>{});
+        }
       });
     });
     if constexpr (DS) {
@@ -269,10 +303,66 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
     // neighbour row, so lane rows 0/2 hold 8 channels of pixel row j, 1/3 of j+1
     const int obase = ((o.b * a.H + o.oy0) * a.W + o.ox0) * (int)(a.out_pstride * 2);  // uniform
 #pragma unroll
-    for (int j = 0; j < 16; j += 2) {
+    for (int j = 0; j < TP; j += 2) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         f32x4 v0 = acc[i][j], v1 = acc[i][j + 1];
+        if constexpr (X3) {
+          // residual hi + lo of logical channels cw + 16 i + 4 fgt .. +3: split
+          // columns 64 (cw / 32) + 16 i + 4 fgt (hi) and + 32 (lo) -- 16-B chunk
+          // ch (hi) / ch + 4 (lo), 8-B half fgt & 1; then ReLU in fp32, hi =
+          // bf16(v), lo = bf16(v - hi), 16-B stores of rows (j, j + 1) paired by
+          // v_permlane16_swap
+          if constexpr (RES) {
+            const int ch = 8 * (cw >> 5) + 2 * i + (fgt >> 1);
+            const int pa = (r0w + j) * 16 + frt;
+            const char* rb0 = smem + OFF_RES + pa * 256 + (fgt & 1) * 8;
+            const char* rb1 = rb0 + 16 * 256;
+            const uint2 h0 = *(const uint2*)(rb0 + ((ch ^ (pa & 15)) << 4));
+            const uint2 l0 = *(const uint2*)(rb0 + (((ch + 4) ^ (pa & 15)) << 4));
+            const uint2 h1 = *(const uint2*)(rb1 + ((ch ^ (pa & 15)) << 4));
+            const uint2 l1 = *(const uint2*)(rb1 + (((ch + 4) ^ (pa & 15)) << 4));
+            v0[0] += __uint_as_float(h0.x << 16) + __uint_as_float(l0.x << 16);
+            v0[1] += __uint_as_float(h0.x & 0xFFFF0000u) + __uint_as_float(l0.x & 0xFFFF0000u);
+            v0[2] += __uint_as_float(h0.y << 16) + __uint_as_float(l0.y << 16);
+            v0[3] += __uint_as_float(h0.y & 0xFFFF0000u) + __uint_as_float(l0.y & 0xFFFF0000u);
+            v1[0] += __uint_as_float(h1.x << 16) + __uint_as_float(l1.x << 16);
+            v1[1] += __uint_as_float(h1.x & 0xFFFF0000u) + __uint_as_float(l1.x & 0xFFFF0000u);
+            v1[2] += __uint_as_float(h1.y << 16) + __uint_as_float(l1.y << 16);
+            v1[3] += __uint_as_float(h1.y & 0xFFFF0000u) + __uint_as_float(l1.y & 0xFFFF0000u);
+          }
+          if (a.relu)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v0[r] = fmaxf(v0[r], 0.f);
+              v1[r] = fmaxf(v1[r], 0.f);
+            }
+          uint32_t qh[4] = {l1b_pk(v0[0], v0[1]), l1b_pk(v0[2], v0[3]), l1b_pk(v1[0], v1[1]), l1b_pk(v1[2], v1[3])};
+          const float vv[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          uint32_t ql[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            ql[e] = l1b_pk(vv[2 * e] - __uint_as_float(qh[e] << 16), vv[2 * e + 1] - __uint_as_float(qh[e] & 0xFFFF0000u));
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const auto rh = __builtin_amdgcn_permlane16_swap(qh[e], qh[e + 2], false, false);
+            qh[e] = rh[0];
+            qh[e + 2] = rh[1];
+            const auto rl = __builtin_amdgcn_permlane16_swap(ql[e], ql[e + 2], false, false);
+            ql[e] = rl[0];
+            ql[e + 2] = rl[1];
+          }
+          const int px = (r0w + j + (fgt & 1)) * a.W + frt;
+          const int pc = 64 * (cw >> 5) + 16 * i + (fgt >> 1) * 8;  // split column of the hi half
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(l1b_v4, make_uint4(qh[0], qh[1], qh[2], qh[3])), ro,
+                                                 px * (int)(a.out_pstride * 2) + pc * 2, obase, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(l1b_v4, make_uint4(ql[0], ql[1], ql[2], ql[3])), ro,
+                                                 px * (int)(a.out_pstride * 2) + (pc + 32) * 2, obase, 0);
+          const f32x4 b0 = biasv(i);
+          acc[i][j] = b0;
+          acc[i][j + 1] = b0;
+          continue;
+        }
         if constexpr (RES) {
           // residual of channels cw + 16 i + 4 fgt .. +3 of pixels (j, frt), (j + 1, frt)
           const int ch = (cw >> 3) + 2 * i + (fgt >> 1);
@@ -311,10 +401,38 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-int launch_l2conv(const BlockConvArgs& a, hipStream_t s) {
+// (x3: the split layout's bf16 channel counts / strides, as launch_block_conv
+// passes them: Cin 128 = 64 logical, Cout and the bias logical 64)
+int launch_l2conv(const BlockConvArgs& a, hipStream_t s, bool x3) {
   using namespace l2c;
   SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.pool_out && !a.st_part,
-              "variant 41: 3x3/s1/p1, no pool or statistics");
+              "variant 41/42: 3x3/s1/p1, no pool or statistics");
+  if (x3) {
+    SAD_REQUIRE(!a.in1 && a.Cin == 128 && a.Cout == 64 && a.H % 16 == 0 && a.W % 16 == 0 && a.Ho == a.H &&
+                    a.Wo == a.W && a.wt_ld >= 9 * 128 && a.wt_ld % 8 == 0 && a.in0_pstride % 64 == 0 &&
+                    a.in0_pstride >= 128 && a.out_pstride % 64 == 0 && a.out_pstride >= 128 &&
+                    (!a.res || (a.res_pstride % 64 == 0 && a.res_pstride >= 128)) && a.out,
+                "variant 42: split-bf16 64 -> 64 logical 3x3/s1/p1 (layer1), 16 x 16 tiles");
+    const int64_t tiles = (int64_t)a.N * (a.H / 16) * (a.W / 16);
+    if (tiles == 0) return SAD_OK;
+    const int64_t g = std::min<int64_t>(tiles, 256);
+    BlockConvArgs b = a;
+    b.out_bytes = ((int64_t)a.N * a.H * a.W - 1) * a.out_pstride * 2 + 256;
+    SAD_REQUIRE(b.out_bytes < (1ll << 31) - 65536, "variant 42: output passes the 32-bit buffer range");
+    static bool attr[2] = {false, false};
+    const void* kfn = a.res ? (const void*)l2conv_kernel<true, false, true> : (const void*)l2conv_kernel<false, false, true>;
+    const int smem = (a.res ? SMEM_RES : OFF_RES) + 512;
+    if (!attr[a.res ? 1 : 0]) {
+      SAD_CHECK_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
+      attr[a.res ? 1 : 0] = true;
+    }
+    if (a.res)
+      hipLaunchKernelGGL((l2conv_kernel<true, false, true>), dim3((unsigned)g), dim3(256), smem, s, b);
+    else
+      hipLaunchKernelGGL((l2conv_kernel<false, false, true>), dim3((unsigned)g), dim3(256), smem, s, b);
+    SAD_CHECK_HIP(hipGetLastError());
+    return SAD_OK;
+  }
   SAD_REQUIRE(!a.in1 || (!a.res && a.Cin1 == 64 && a.ss1 == 2 && a.H1 == 2 * a.H && a.W1 == 2 * a.W &&
                          a.in1_pstride % 8 == 0 && a.wt_ld >= 9 * 128 + 64),
               "variant 41: the shortcut is a 1x1/2 downsample of a 64-channel input at twice the size");

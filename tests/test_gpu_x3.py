@@ -94,11 +94,16 @@ def test_block_conv_x3_vs_float64(cin, cout, H, stride, shortcut, variant):
 
 @pytest.mark.parametrize('c,H,res,variant', [(64, 32, True, 20), (64, 48, False, 20), (128, 16, True, 20),
                                              (128, 32, False, 20), (64, 32, True, 26), (64, 48, False, 26),
-                                             (64, 16, True, 26), (64, 80, True, 26)])
+                                             (64, 16, True, 26), (64, 80, True, 26),
+                                             # variant 42 (round 4): the parity mode's layer1 default
+                                             (64, 32, True, 42), (64, 48, False, 42), (64, 16, True, 42),
+                                             (64, 80, True, 42), (64, 160, True, 42), (64, 160, False, 42)])
 def test_halo_conv_x3_vs_float64(c, H, res, variant):
     """The split-bf16 halo kernels (variant 20: weight ring, layer2 stride-1
     convs; variant 26: resident weights, half the channels per workgroup,
-    layer1) with the identity shortcut as an epilogue residual, vs float64."""
+    layer1; variant 42: register-resident weights, all channels per workgroup,
+    layer1) with the identity shortcut as an epilogue residual, vs float64
+    (H = 160: 300 tiles, more than workgroups)."""
     from sad.engine import block_conv, from_split, to_split
     g = torch.Generator().manual_seed(c + H + int(res))
     N = 3

@@ -78,6 +78,8 @@ def main():
     g0 = step(base, head, img, tg)
     rows = [('forward activations bf16', dict(fwd=True)), ('backward gradients bf16', dict(bwd=True)),
             ('forward bf16 except layer4', dict(fwd=True, skip=lambda n, m: n.startswith('layer4'))),
+            # the trainer's mixed mode (round 4): stem + layers 1-3 fp32, layer4 bf16 (forward and backward)
+            ('layer4 fwd+bwd bf16 only', dict(fwd=True, bwd=True, skip=lambda n, m: not n.startswith('layer4'))),
             ('conv outputs bf16 only', dict(fwd=True, skip=lambda n, m: not isinstance(m, torch.nn.Conv2d))),
             ('BN/ReLU outputs bf16 only', dict(fwd=True, skip=lambda n, m: isinstance(m, torch.nn.Conv2d)))]
     for tag, kw in rows:
