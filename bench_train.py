@@ -36,7 +36,7 @@ def main():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch-size', type=int, default=32, help='files per GPU per step (2 segments each)')
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'mixed', 'fp32'])
     ap.add_argument('--pool', type=int, default=256, help='synthetic training clips per rank')
     ap.add_argument('--eval-clips', type=int, default=64)
     ap.add_argument('--lr', type=float, default=1e-3)

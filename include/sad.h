@@ -435,6 +435,10 @@ int sad_adamw_run(float* p, const float* g, float* m, float* v, int64_t n, float
 /* y += alpha * x (fp32): folds a step's layer3 gradient into its never-zeroed
  * .grad (quirk C4: layer3 is unfrozen at epochs//3 but not in the optimizer). */
 int sad_axpy_run(float* y, const float* x, int64_t n, float alpha, void* stream);
+/* Element-wise dtype conversion fp32 <-> bf16 (RNE) of n values: the mixed
+ * trainer's hand-over between its fp32 frozen prefix (stem, layers 1-3) and
+ * its bf16 layer4 (sad/train.py, submodel_trainer.py --precision mixed). */
+int sad_cast_run(const void* src, int32_t src_dtype, void* dst, int32_t dst_dtype, int64_t n, void* stream);
 /* timm global average pool: x NHWC [B, hw, C] (dtype) -> out [B, C] fp32 (the
  * trainer's model(inputs), quirk C1). */
 int sad_avgpool_run(const void* x, int64_t B, int32_t hw, int32_t C, int32_t dtype, float* out, void* stream);

@@ -1068,6 +1068,54 @@ extern "C" int sad_axpy_run(float* y, const float* x, int64_t n, float alpha, vo
   return SAD_OK;
 }
 
+// 8 elements per thread: fp32 -> bf16 (one v_cvt_pk_bf16_f32 per pair) or bf16 -> fp32
+template <bool TO_BF16>
+__global__ void cast_kernel(const void* __restrict__ src, void* __restrict__ dst, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n) return;
+  if constexpr (TO_BF16) {
+    const float* s = (const float*)src + i;
+    u16* d = (u16*)dst + i;
+    if (i + 8 <= n) {
+      const float4 a = *(const float4*)s, b = *(const float4*)(s + 4);
+      *(uint4*)d = make_uint4((uint32_t)f2bf(a.x) | ((uint32_t)f2bf(a.y) << 16),
+                              (uint32_t)f2bf(a.z) | ((uint32_t)f2bf(a.w) << 16),
+                              (uint32_t)f2bf(b.x) | ((uint32_t)f2bf(b.y) << 16),
+                              (uint32_t)f2bf(b.z) | ((uint32_t)f2bf(b.w) << 16));
+    } else {
+      for (int64_t k = i; k < n; ++k) ((u16*)dst)[k] = f2bf(((const float*)src)[k]);
+    }
+  } else {
+    const u16* s = (const u16*)src + i;
+    float* d = (float*)dst + i;
+    if (i + 8 <= n) {
+      const uint4 q = *(const uint4*)s;
+      *(float4*)d = make_float4(bf2f((u16)(q.x & 0xFFFF)), bf2f((u16)(q.x >> 16)), bf2f((u16)(q.y & 0xFFFF)),
+                                bf2f((u16)(q.y >> 16)));
+      *(float4*)(d + 4) = make_float4(bf2f((u16)(q.z & 0xFFFF)), bf2f((u16)(q.z >> 16)), bf2f((u16)(q.w & 0xFFFF)),
+                                      bf2f((u16)(q.w >> 16)));
+    } else {
+      for (int64_t k = i; k < n; ++k) ((float*)dst)[k] = bf2f(((const u16*)src)[k]);
+    }
+  }
+}
+
+extern "C" int sad_cast_run(const void* src, int32_t src_dtype, void* dst, int32_t dst_dtype, int64_t n, void* stream) {
+  SAD_REQUIRE(src && dst && n >= 0, "bad args");
+  SAD_REQUIRE((src_dtype == SAD_F32 && dst_dtype == SAD_BF16) || (src_dtype == SAD_BF16 && dst_dtype == SAD_F32),
+              "cast: fp32 <-> bf16 only");
+  SAD_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "cast: 16-B aligned buffers");
+  if (!n) return SAD_OK;
+  const int64_t th = (n + 7) / 8;
+  const dim3 grid((unsigned)((th + 255) / 256));
+  if (src_dtype == SAD_F32)
+    hipLaunchKernelGGL(cast_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, src, dst, n);
+  else
+    hipLaunchKernelGGL(cast_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, src, dst, n);
+  SAD_CHECK_HIP(hipGetLastError());
+  return SAD_OK;
+}
+
 extern "C" int sad_avgpool_run(const void* x, int64_t B, int32_t hw, int32_t C, int32_t dtype, float* out,
                                void* stream) {
   SAD_REQUIRE(x && out && B >= 0 && hw > 0 && C % 64 == 0, "bad args (C must be a multiple of 64)");

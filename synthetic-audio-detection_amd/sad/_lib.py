@@ -124,6 +124,7 @@ SIGNATURES = {
                                           ctypes.c_float, ctypes.c_float, I64, ctypes.POINTER(PackSeg), I32, I32,
                                           P]),
     'sad_axpy_run': (ctypes.c_int, [P, P, I64, ctypes.c_float, P]),
+    'sad_cast_run': (ctypes.c_int, [P, I32, P, I32, I64, P]),
     'sad_avgpool_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, P]),
 }
 

@@ -32,7 +32,9 @@ Differences (documented in DESIGN.md / INTEGRATION.md):
     per-replica BN statistics as in DP; gradients all-reduced.
   * no CPU fallback; ``--model-name`` must be a BasicBlock ResNet (resnet18,
     resnet34): the device backward kernels implement timm's BasicBlock.
-  * extra flags: ``--precision {bf16,fp32}`` (default bf16 = throughput mode),
+  * extra flags: ``--precision {bf16,mixed,fp32}`` (default bf16 = throughput
+    mode; mixed = the frozen stem/layers 1-3 in fp32 and layer4 in bf16, whose
+    layer4 gradients track fp32 autograd to cosine >= 0.95),
     ``--max-steps`` (stop an epoch early; benchmarking).
   * TensorBoard is optional (not installed here): scalars are logged instead.
 """
@@ -86,8 +88,9 @@ def parse_args(argv=None):
     parser.add_argument('--Class1', default='Class1', type=str, help='Name of Class 1 eg. Training platform')
     parser.add_argument('--model-name', default='resnet18', type=str, choices=RESNET_MODELS,
                         help='Name of model to use')
-    parser.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'],
-                        help='device compute precision (fp32 = the reference arithmetic)')
+    parser.add_argument('--precision', default='bf16', choices=['bf16', 'mixed', 'fp32'],
+                        help='device compute precision (fp32 = the reference arithmetic; mixed = fp32 frozen prefix '
+                             '+ bf16 layer4)')
     parser.add_argument('--max-steps', default=0, type=int, help='stop each epoch after this many steps (0 = all)')
     return parser.parse_args(argv)
 

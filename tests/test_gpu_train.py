@@ -332,3 +332,57 @@ def test_train_step_resnet50_bf16_runs():
     print(f'resnet50 bf16 loss {o["loss"]:.5f} vs {o["rloss"]:.5f}; layer4 grad cosine {total:.4f}, per block '
           + ', '.join(f'{b} {c:.4f}' for b, c in per.items()))
     assert per['layer4.2'] >= 0.9 and total >= 0.6
+
+
+def _cosines(o, prefix='layer4.'):
+    return {n: torch.nn.functional.cosine_similarity(o['g'][n].flatten().double(), gr.flatten().double(),
+                                                     dim=0).item()
+            for n, gr in o['rg'].items() if n.startswith(prefix)}
+
+
+def test_train_step_resnet50_mixed_gradient_gate():
+    """--precision mixed (sad.train.MixedNet: stem + layers 1-3 in fp32, layer4
+    in bf16, forward and backward) is the bf16 trainer whose gradients track
+    fp32 autograd: EVERY layer4 parameter tensor's gradient cosine >= 0.95 on
+    resnet50 (bf16 throughput mode: 0.93 / 0.70 / 0.62 per block; the CPU
+    emulation of the mixed arithmetic, tools/bf16_grad_emulation.py, gives a
+    per-tensor minimum of 0.983), loss within 1e-2; then a step with layer3
+    unfrozen (quirk C4: its gradient crosses back from the bf16 layer4 into the
+    fp32 layer3 through sad_cast_run) with the same bar on layer3's tensors."""
+    from sad import train as st
+    from sad import weights as sw
+    sd = (sw.backbone_state_dict(7, 'resnet50'), st.init_state_dict(42, 'resnet50')[1])
+    tr, m, out = _run_steps(sd, 'mixed', 2, unfreeze_at=1, model_name='resnet50')
+    assert isinstance(tr.net, st.MixedNet)
+    for k, o in enumerate(out):
+        c4 = _cosines(o, 'layer4.')
+        c3 = _cosines(o, 'layer3.')
+        worst = min(c4.items(), key=lambda kv: kv[1])
+        print(f"resnet50 mixed step {k}: loss {o['loss']:.5f} vs {o['rloss']:.5f}; layer4 min per-tensor cosine "
+              f"{worst[1]:.4f} ({worst[0]})" + (f"; layer3 min {min(c3.values()):.4f}" if c3 else ''))
+        assert abs(o['loss'] - o['rloss']) <= 1e-2 * abs(o['rloss'])
+        assert len(c4) == len([n for n in tr.net.names if n.startswith('layer4.')])
+        assert worst[1] >= 0.95, worst
+        assert (len(c3) > 0) == (k >= 1)
+        if c3:
+            assert min(c3.values()) >= 0.95, min(c3.items(), key=lambda kv: kv[1])
+    # the frozen prefix is never stepped; layer4 moved
+    for name, p in m.base.named_parameters():
+        if name.startswith('layer3.'):
+            assert torch.equal(tr.net.params[name].cpu(), p.detach())
+
+
+def test_train_step_resnet18_mixed(model_sd):
+    """resnet18 in the mixed precision: loss within 1e-3 relative of autograd and
+    every layer4 tensor's gradient cosine >= 0.99; running statistics of the
+    fp32 prefix as fp32's (<= 1e-4)."""
+    tr, m, out = _run_steps(model_sd, 'mixed', 1)
+    o = out[0]
+    c4 = _cosines(o)
+    print(f"resnet18 mixed loss {o['loss']:.6f} vs {o['rloss']:.6f}; min cosine {min(c4.values()):.5f}")
+    assert abs(o['loss'] - o['rloss']) <= 1e-3 * abs(o['rloss'])
+    assert min(c4.values()) >= 0.99
+    sd = tr.net.base_state_dict()
+    for k in ('layer2.1.bn1', 'layer3.0.downsample.1'):
+        bn = m.base.get_submodule(k)
+        assert _rel(sd[f'{k}.running_var'], bn.running_var) <= 1e-4
