@@ -1020,7 +1020,8 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   if (a.wt_ld == 0) a.wt_ld = a.KH * a.KW * a.Cin + (a.in1 ? a.Cin1 : 0);
   SAD_REQUIRE(a.wt_ld >= a.KH * a.KW * a.Cin + (a.in1 ? a.Cin1 : 0) && (a.wt_ld * ES) % 16 == 0, "weight row length");
   a.wt_bytes = (int64_t)a.Cout * a.wt_ld * ES;
-  a.res_bytes = a.res ? (a.M - 1) * a.res_pstride * ES + a.Cout * ES : 0;
+  // (split-bf16: a pixel's residual is 2 Cout bf16, hi and lo -- Cout stays logical)
+  a.res_bytes = a.res ? (a.M - 1) * a.res_pstride * ES + (dtype == SAD_BF16X3 ? 2 : 1) * a.Cout * ES : 0;
   // The kernels address their operands through 32-bit buffer offsets.  A batch
   // whose operands exceed that range runs as consecutive launches over image
   // ranges (every conv here is independent per image, so the results are the

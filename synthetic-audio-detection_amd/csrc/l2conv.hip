@@ -263,6 +263,40 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
         if constexpr (!X3) {
           mm(std::integral_constant<int, 0>{}, std::integral_constant<int, s>{});
           mm(std::integral_constant<int, 1>{}, std::integral_constant<int, s>{});
+        } else if constexpr (u == NUC - 2) {
+          // the chunk's last fragment (both its units) as ONE asm statement
+          // ending in the 8-pass XDL result wait: hipcc does not pad for asm
+          // MFMAs, and around the chunk end its register allocator moves
+          // accumulators (v_mov) -- inside one statement it cannot, and after
+          // it the results are complete (tools/asm_hazards.py audits this)
+          const uint4 xl = bq[(u + 1) % DQ];
+          static_assert(j == TP - 1 && h == 0, "last fragment");
+          if constexpr (s_hi >= NS - WV)
+            asm volatile(
+                "v_mfma_f32_16x16x32_bf16 %0, %2, %6, %0\n\t"
+                "v_mfma_f32_16x16x32_bf16 %1, %3, %6, %1\n\t"
+                "v_mfma_f32_16x16x32_bf16 %0, %4, %6, %0\n\t"
+                "v_mfma_f32_16x16x32_bf16 %1, %5, %6, %1\n\t"
+                "v_mfma_f32_16x16x32_bf16 %0, %2, %7, %0\n\t"
+                "v_mfma_f32_16x16x32_bf16 %1, %3, %7, %1\n\t"
+                "s_nop 11"
+                : "+v"(acc[0][j]), "+v"(acc[1][j])
+                : "a"(wr[0][s_hi]), "v"(wr[1][s_hi]), "a"(wr[0][s_lo]), "v"(wr[1][s_lo]),
+                  "v"(__builtin_bit_cast(l1b_v4, bf)), "v"(__builtin_bit_cast(l1b_v4, xl)));
+          else
+            asm volatile(
+                "v_mfma_f32_16x16x32_bf16 %0, %2, %6, %0\n\t"
+                "v_mfma_f32_16x16x32_bf16 %1, %3, %6, %1\n\t"
+                "v_mfma_f32_16x16x32_bf16 %0, %4, %6, %0\n\t"
+                "v_mfma_f32_16x16x32_bf16 %1, %5, %6, %1\n\t"
+                "v_mfma_f32_16x16x32_bf16 %0, %2, %7, %0\n\t"
+                "v_mfma_f32_16x16x32_bf16 %1, %3, %7, %1\n\t"
+                "s_nop 11"
+                : "+v"(acc[0][j]), "+v"(acc[1][j])
+                : "a"(wr[0][s_hi]), "a"(wr[1][s_hi]), "a"(wr[0][s_lo]), "a"(wr[1][s_lo]),
+                  "v"(__builtin_bit_cast(l1b_v4, bf)), "v"(__builtin_bit_cast(l1b_v4, xl)));
+        } else if constexpr (u == NUC - 1) {
+          // (issued with the previous unit)
         } else if constexpr (h == 0) {  // the hi fragment: W_hi.X_hi, W_lo.X_hi
           mm(std::integral_constant<int, 0>{}, std::integral_constant<int, s_hi>{});
           mm(std::integral_constant<int, 1>{}, std::integral_constant<int, s_hi>{});
