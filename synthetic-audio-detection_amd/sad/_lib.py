@@ -140,7 +140,12 @@ def load():
                                f'`python -c "import __graft_entry__ as g; g.build()"`')
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            # (an older build loaded for a same-box A/B may lack newer entry
+            # points: they fail when called; tests/test_abi.py checks the
+            # in-tree build exports every one)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
             fn.restype = res
             fn.argtypes = args
         _lib = lib
