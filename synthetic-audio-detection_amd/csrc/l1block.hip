@@ -85,7 +85,7 @@ constexpr int QSKIP = 10;                  // pieces 0-9 = patch rows 0-3: a con
 constexpr int NS = 18;                     // K-steps per conv: 9 taps x 2 halves of 32 channels
 constexpr int NU1 = NS * NF;               // conv1 (read, 2 MFMA) units per wave
 constexpr int NU2 = NS * 8;                // conv2 units per wave
-constexpr int DQ = 6;                      // fragment reads in flight ahead of their MFMAs
+constexpr int DQ = 10;                     // fragment reads in flight ahead of their MFMAs (round 4: 6 -> 10)
 constexpr int SA = 6;                      // conv1 K-steps run K-step-outer (the rest fragment-outer)
 constexpr int NB1 = NS - SA;
 constexpr int W2V = 8;                     // conv2 K-steps of channel tile 1 whose weights sit in VGPRs

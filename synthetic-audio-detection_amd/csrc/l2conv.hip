@@ -77,6 +77,7 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
   constexpr int UPT = 2 * TP;           // units per tap: (fragment, K-half)
   constexpr int NUC = 9 * UPT;          // units per chunk
   constexpr int PDIV = X3 ? 8 : 16;     // units between patch DMA pieces
+  constexpr int DQ = X3 ? 8 : l2c::DQ;  // fragment reads in flight (X3: 143 VGPRs leave room)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);

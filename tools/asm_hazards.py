@@ -9,9 +9,11 @@ reader other than the next MFMA taking it whole as C
 (/opt/skills/guides/cdna_hip_programming.md, inline-asm rule 2).
 
 Scans every kernel of the given sources (hipcc -S for gfx950) linearly: for each
-inline-asm v_mfma (between ;;#ASMSTART / ;;#ASMEND; hipcc pads its own), the instructions in the following 12 wait states (one per instruction,
-N + 1 per s_nop N) must not read or write its destination registers, except an
-MFMA whose C and D are exactly that range (an accumulation chain).  Prints the
+inline-asm v_mfma (between ;;#ASMSTART / ;;#ASMEND; hipcc pads its own), the
+instructions in the following 12 wait states (one per instruction, N + 1 per
+s_nop N, 4 per intervening MFMA -- the wave cannot issue it before the XDL pipe
+frees, >= 16 cycles) must not read or write its destination registers, except
+an MFMA whose C and D are exactly that range (an accumulation chain).  Prints the
 violations; exit status 1 if any.
 
     python tools/asm_hazards.py synthetic-audio-detection_amd/csrc/l1block.hip ...
@@ -88,6 +90,12 @@ def audit(body):
                 d2, a2, b2, c2 = regs(o2[0]), regs(o2[1]), regs(o2[2]), regs(o2[3]) if len(o2) > 3 else set()
                 if (a2 | b2) & dst or ((c2 & dst) and not (c2 == dst and d2 == dst)) or ((d2 & dst) and d2 != dst):
                     bad.append((i, ins, nxt, states))
+                # an intervening MFMA holds the wave >= 16 cycles (the XDL pipe
+                # is busy with the one before it): counted as 4 wait states
+                states += 4
+                if states >= STATES:
+                    break
+                continue
             elif regs(nxt) & dst:
                 bad.append((i, ins, nxt, states))
             states += 1
