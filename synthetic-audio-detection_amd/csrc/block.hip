@@ -703,6 +703,7 @@ int launch_l2conv(const BlockConvArgs& a, hipStream_t s, bool x3 = false);
 int launch_halo256s2(const BlockConvArgs& a, hipStream_t s);
 bool halo256s2_ok(const BlockConvArgs& a);
 int launch_halo_rw_x3(const BlockConvArgs& a, hipStream_t s);
+int launch_l2s2conv(const BlockConvArgs& a, hipStream_t s);
 
 // halo kernel (variant 20): bf16 stride-1 3x3 with Cout <= 128 (layer1, layer2's
 // second block), where the implicit GEMM is L2->LDS-fill bound (convbench,
@@ -787,6 +788,22 @@ static bool s2_patch() {
     return e ? atoi(e) != 0 : false;
   }();
   return v;
+}
+// SAD_L2S2_RW=0 runs layer2.0's stride-2 conv1 (64 -> 128) on the implicit
+// GEMM (variant 15) instead of the resident-weight stride-2 conv (variant 43,
+// l2s2conv.hip; A/B switch)
+static bool l2s2_rw() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_L2S2_RW");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+// variant 43's contract: 64 -> 128 3x3/s2/p1, output tiles 16 x 16, input
+// exactly twice the output, no shortcut / residual / pool / statistics
+static bool l2s2_ok(const BlockConvArgs& a) {
+  return a.KH == 3 && a.KW == 3 && a.stride == 2 && a.pad == 1 && a.Cin == 64 && a.Cout == 128 && a.Ho % 16 == 0 &&
+         a.Wo % 16 == 0 && a.H == 2 * a.Ho && a.W == 2 * a.Wo && !a.in1 && !a.res && !a.pool_out && !a.st_part;
 }
 bool layer2_halo() {
   static const bool v = [] {
@@ -890,6 +907,9 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   // micro-batch (a 1-rank and a 2-rank run of the same segments must agree
   // bit for bit)
   if (dtype == SAD_BF16 && halo256_mode() != 0 && halo256_ok(a)) return halo256_mode() == 2 ? 31 : 30;
+  // layer2's stride-2 conv1 (64 -> 128): resident weights (variant 43; chosen
+  // whatever the grid size: its K order differs from variant 15's)
+  if (dtype == SAD_BF16 && l2s2_rw() && l2s2_ok(a)) return 43;
   // the stride-2 3x3 convs: the patch-resident variant 32 (chosen whatever the
   // grid size, as above)
   if (dtype == SAD_BF16 && s2_patch() && halo256s2_ok(a)) return 32;
@@ -926,7 +946,7 @@ static bool variant_fits(int v, int cout) {
   if (v == 20 || v == 21) return cout % 64 == 0;
   if (v == 22) return cout % 128 == 0;
   if (v == 25) return cout == 64;
-  if (v == 41) return cout == 128;
+  if (v == 41 || v == 43) return cout == 128;
   return v >= 9 && v <= 19 && cout % bc[v] == 0;
 }
 
@@ -1092,6 +1112,10 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   if (v == 41) {
     SAD_REQUIRE(dtype == SAD_BF16 && (halo_ok(a_in, dtype) || l2conv_ds_ok(a_in)), "variant 41: bf16 3x3/s1/p1, H, W % 16");
     return launch_l2conv(a, s);
+  }
+  if (v == 43) {
+    SAD_REQUIRE(dtype == SAD_BF16 && l2s2_ok(a_in), "variant 43: bf16 64 -> 128 3x3/s2/p1, output H, W % 16");
+    return launch_l2s2conv(a, s);
   }
   if (v == 42) {
     SAD_REQUIRE(dtype == SAD_BF16X3 && halo_ok(a_in, dtype) && a_in.Cin == 64 && a_in.Cout == 64,

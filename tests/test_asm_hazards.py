@@ -13,7 +13,7 @@ import pytest
 from conftest import PKG, ROOT
 
 
-@pytest.mark.parametrize('src', ['l1block.hip', 'l2conv.hip'])
+@pytest.mark.parametrize('src', ['l1block.hip', 'l2conv.hip', 'l2s2conv.hip'])
 def test_no_mfma_result_hazards(src):
     sys.path.insert(0, os.path.join(ROOT, 'tools'))
     import asm_hazards

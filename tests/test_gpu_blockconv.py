@@ -107,6 +107,12 @@ CASES = [
     ('l4-s2-32', 5, 32, 256, 512, 2, None, [32]),
     ('l3-s2-32-ragged', 70, 32, 128, 256, 2, None, [32]),
     ('l4-s2-32-many', 300, 32, 256, 512, 2, None, [32]),
+    # variant 43 (resident-weight 64 -> 128 stride-2 conv, l2s2conv.hip):
+    # layer2.0's conv1; one tile per image (both padded edges in one tile), fewer
+    # tiles than workgroups, more (320 on 256: two per workgroup on some)
+    ('l2-s2-43-one-tile', 3, 32, 64, 128, 2, None, [43]),
+    ('l2-s2-43', 2, 128, 64, 128, 2, None, [43]),
+    ('l2-s2-43-many', 20, 128, 64, 128, 2, None, [43]),
 ]
 
 

@@ -1,8 +1,8 @@
-"""CPU: the LDS layouts of the layer2 resident-weight conv (csrc/l2conv.hip,
-variant 41: its conv patch, residual tile and downsample patch) and of the
-stride-2 patch kernel
-(csrc/halo256s2.hip, variant 32), checked exhaustively with the kernels' own
-index formulas.
+"""CPU: the LDS layouts of the layer2 resident-weight convs (csrc/l2conv.hip,
+variant 41: its conv patch, residual tile and downsample patch; csrc/l2s2conv.hip,
+variant 43: the stride-2 conv1's row-half patch) and of the stride-2 patch
+kernel (csrc/halo256s2.hip, variant 32), checked exhaustively with the kernels'
+own index formulas.
 
 * every ds_read_b128 fragment read is free of LDS bank conflicts under the
   MI355X ds_read_b128 lane grouping (MI355X_MICROARCH.md, LDS table: 4 groups
@@ -176,3 +176,60 @@ def test_l2conv_residual_reads_consistent():
                         assert px == pa and chunk * 8 + (fgt & 1) * 4 == cw + 16 * i + 4 * fgt
                     worst = max(worst, lds_cycles_b64(addrs))
     assert worst <= 4  # 2 LDS cycles minimum for a b64 read; the epilogue's reads are off the MFMA path
+
+
+# ---- variant 43 (csrc/l2s2conv.hip): a row-half's 17 x 33 input patch x 64
+# channels, rows de-interleaved (even rows 0..16 first, then odd rows 1..15),
+# per row the 17 even columns then the 16 odd ones, 128 B each, 16-B chunk c of
+# plane column x' at c ^ key(x')
+KEY43, ROWB43, ODDC43, NEV43, NPX43 = 0x7929284ef1797, 33 * 128, 17 * 128, 9, 17 * 33
+
+
+def key43(x):
+    return (KEY43 >> (3 * x)) & 7
+
+
+def l2s2_write_map():
+    """LDS byte offset -> (patch row Y, patch column X, source chunk) or None,
+    from the kernel's per-piece formulas (pixel slot u = 8q + ln / 8)."""
+    m = {}
+    for q in range((NPX43 * 128 + 1023) // 1024):
+        for ln in range(64):
+            u = 8 * q + (ln >> 3)
+            r = (u * 1986) >> 16
+            assert r == u // 33
+            cu = u - 33 * r
+            Y = 2 * r if r < NEV43 else 2 * (r - NEV43) + 1
+            odd = cu >= 17
+            xp = cu - 17 if odd else cu
+            X = 2 * xp + (1 if odd else 0)
+            m[q * 1024 + ln * 16] = (Y, X, (ln & 7) ^ key43(xp)) if u < NPX43 else None
+    return m
+
+
+def test_l2s2_patch_covers_window():
+    wm = l2s2_write_map()
+    got = [v for v in wm.values() if v is not None]
+    assert len(got) == len(set(got))
+    assert set(got) == {(y, x, c) for y in range(17) for x in range(33) for c in range(8)}
+
+
+def test_l2s2_reads_conflict_free_and_consistent():
+    wm = l2s2_write_map()
+    for ky in range(3):
+        for kx in range(3):
+            for kh in range(2):
+                for j in range(8):
+                    addrs = []
+                    for lane in range(64):
+                        fr, fg = lane & 15, lane >> 4
+                        xp = fr + (1 if kx == 2 else 0)
+                        L = (ODDC43 if kx == 1 else 0) + xp * 128 + (((4 * kh + fg) ^ key43(xp)) << 4)
+                        base = L + (NEV43 * ROWB43 if ky == 1 else 0)
+                        row = j if ky == 1 else j + ky // 2
+                        a = base + row * ROWB43
+                        addrs.append(a)
+                        # output row j of the half, column fr reads patch (2 j + ky, 2 fr + kx),
+                        # channels (4 kh + fg) * 8 .. + 7
+                        assert wm[a] == (2 * j + ky, 2 * fr + kx, 4 * kh + fg), (ky, kx, kh, j, lane)
+                    assert lds_cycles(addrs) == 4, (ky, kx, kh, j)
