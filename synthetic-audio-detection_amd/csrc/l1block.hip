@@ -333,14 +333,23 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
       auto prefix = [&](bool left) __attribute__((always_inline)) {
         const int y = left ? (frt >> 1) & 1 : pg;
         f32x4 pa[2];
-#pragma unroll
-        for (int st = 0; st < NS; ++st) {
+        auto rdp = [&](int st) __attribute__((always_inline)) {
           const int tap = st >> 1, h = st & 1, ky = tap / 3, kx = tap % 3;
           const int Y = y + ky;
           const int ad = left ? pbo + (Y * PWD + 16 + et + kx) * 128 +
                                     ((KXt[kx] ^ ((Y & 3) << 1) ^ (h << 2)) << 4)
                               : pbo + (LAt[kx] ^ (((Y & 3) << 5) ^ (h << 6))) + Y * PROW;
-          const uint4 bf = *(const uint4*)(smem + ad);
+          return *(const uint4*)(smem + ad);
+        };
+        // 4 fragment reads in flight (a read per 2 dependent MFMAs would
+        // otherwise wait out the LDS latency every K-step)
+        uint4 pq[4];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) pq[st] = rdp(st);
+#pragma unroll
+        for (int st = 0; st < NS; ++st) {
+          const uint4 bf = pq[st & 3];
+          if (st + 4 < NS) pq[st & 3] = rdp(st + 4);
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             if (st == 0)
@@ -416,17 +425,26 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
     for (int i = 0; i < 2; ++i)
       LRr[i] = (fr2 + 2) * 128 + ((((cw >> 3) + 2 * i + (fg2 >> 1)) ^ l1b_key(fr2 + 2)) << 4) + (fg2 & 1) * 8;
     f32x4 acc2[2][8];
-    auto init2 = [&](auto jc, auto ic) __attribute__((always_inline)) {
+    // in two halves: the bias and residual reads are issued a few units before
+    // the adds that consume them, so the wait for them is not a wait for the
+    // youngest LDS read (lgkmcnt(0) would drain the fragment reads in flight)
+    f32x4 i2b[2];
+    uint2 i2r[2];
+    auto init2_rd = [&](auto jc, auto ic) __attribute__((always_inline)) {
       constexpr int jj = decltype(jc)::value, i = decltype(ic)::value;
-      {
-        const f32x4 b4 = *(const f32x4*)(smem + OFF_B + 256 + (cw + 16 * i + fg2 * 4) * 4);
-        const uint2 rv = *(const uint2*)(smem + ((LRr[i] ^ (((jj + 2) & 3) << 5)) + pbo + pg * 8 * PROW) +
-                                         (jj + 2) * PROW);
-        acc2[i][jj][0] = b4[0] + __uint_as_float(rv.x << 16);
-        acc2[i][jj][1] = b4[1] + __uint_as_float(rv.x & 0xFFFF0000u);
-        acc2[i][jj][2] = b4[2] + __uint_as_float(rv.y << 16);
-        acc2[i][jj][3] = b4[3] + __uint_as_float(rv.y & 0xFFFF0000u);
-      }
+      i2b[i] = *(const f32x4*)(smem + OFF_B + 256 + (cw + 16 * i + fg2 * 4) * 4);
+      i2r[i] = *(const uint2*)(smem + ((LRr[i] ^ (((jj + 2) & 3) << 5)) + pbo + pg * 8 * PROW) + (jj + 2) * PROW);
+    };
+    auto init2_add = [&](auto jc, auto ic) __attribute__((always_inline)) {
+      constexpr int jj = decltype(jc)::value, i = decltype(ic)::value;
+      acc2[i][jj][0] = i2b[i][0] + __uint_as_float(i2r[i].x << 16);
+      acc2[i][jj][1] = i2b[i][1] + __uint_as_float(i2r[i].x & 0xFFFF0000u);
+      acc2[i][jj][2] = i2b[i][2] + __uint_as_float(i2r[i].y << 16);
+      acc2[i][jj][3] = i2b[i][3] + __uint_as_float(i2r[i].y & 0xFFFF0000u);
+    };
+    auto init2 = [&](auto jc, auto ic) __attribute__((always_inline)) {
+      init2_rd(jc, ic);
+      init2_add(jc, ic);
     };
     init2(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
     init2(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
@@ -496,16 +514,22 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
           l1b_mfma_a(acc2[i][jj], w2r[i][s], bf);
       });
       // fragment jj-1's epilogue parts after units 2, 4, 6, 8 of fragment jj,
-      // fragment jj+1's accumulator init after units 10 and 12
-      // (pinned between the MFMAs, as conv1's epilogue parts)
+      // fragment jj+1's accumulator init: its reads after units 5 and 7, the
+      // adds after units 11 and 13 (pinned between the MFMAs, as conv1's
+      // epilogue parts)
       if constexpr (jj >= 1 && s >= 2 && s <= 8 && s % 2 == 0) {
         __builtin_amdgcn_sched_barrier(0);
         epi2(std::integral_constant<int, jj - 1>{}, std::integral_constant<int, s / 2 - 1>{});
         __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (jj + 1 < 8 && (s == 10 || s == 12)) {
+      if constexpr (jj + 1 < 8 && (s == 5 || s == 7)) {
         __builtin_amdgcn_sched_barrier(0);
-        init2(std::integral_constant<int, jj + 1>{}, std::integral_constant<int, (s - 10) / 2>{});
+        init2_rd(std::integral_constant<int, jj + 1>{}, std::integral_constant<int, (s - 5) / 2>{});
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (jj + 1 < 8 && (s == 11 || s == 13)) {
+        __builtin_amdgcn_sched_barrier(0);
+        init2_add(std::integral_constant<int, jj + 1>{}, std::integral_constant<int, (s - 11) / 2>{});
         __builtin_amdgcn_sched_barrier(0);
       }
     });
