@@ -56,7 +56,7 @@ DOMINANT_KERNEL_PREFIX = 'sad::halo256r_kernel<'
 DOMINANT_DESC = ('sad::halo256r_kernel (variant 31): patch-resident 256-channel x 16x16-pixel conv, weights '
                  'streamed into registers; the 12 stride-1 layer3/4 convs of a step (stride-2 convs stay on the '
                  '256x256 implicit GEMM, variant 13)')
-TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r03_pmc_traffic.json', 'r02s3_pmc_traffic_final.json')
+TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r04_pmc_traffic.json', 'r03_pmc_traffic.json')
                      if os.path.exists(os.path.join(ROOT, 'profiles', f))), '')
 FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats
 FE_BYTES = 256000 + 128512     # int16 PCM read + fp32 [128, 251] map written

@@ -81,10 +81,7 @@ __device__ __forceinline__ uint32_t h31_relu2(uint32_t x) {
 // both weight halves on the hi fragment) + W_hi.X_lo (half 1): 96 MFMAs per
 // K-step and wave on the same operand reads and weight loads as bf16's 64; the
 // epilogue splits the fp32 result into hi / lo again.
-// RA > 0 (round 4): a K-step's 2 TP fragment reads run as one rolling window
-// RA reads ahead of their MFMAs across both K-halves (RA = 0: per half, 4 ahead,
-// so each half's first reads wait for nothing to cover them)
-template <int BC, bool POOL, bool X3 = false, int RA = 0>
+template <int BC, bool POOL, bool X3 = false>
 __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   using namespace h31;
   constexpr int NCG = BC / 32, NPG = NW / NCG, TP = 16 / NPG;
@@ -241,36 +238,8 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 4 * NM * TC, 0);
     };
-    if constexpr (RA == 0) {
-      half(std::integral_constant<int, 0>{});
-      half(std::integral_constant<int, 1>{});
-    } else {
-      // unit u = (half u / TP, fragment u % TP): one read, NM * TC MFMAs
-      auto rdu = [&](auto uc) __attribute__((always_inline)) -> uint4 {
-        constexpr int u = decltype(uc)::value;
-        return *(const uint4*)((u / TP ? pb1 : pb0) + (u % TP) * ROWB);
-      };
-      uint4 bq[RA];
-      l1b_for<RA>([&](auto uc) __attribute__((always_inline)) { bq[decltype(uc)::value] = rdu(uc); });
-      l1b_for<2 * TP>([&](auto uc) __attribute__((always_inline)) {
-        constexpr int u = decltype(uc)::value, h = u / TP, j = u % TP;
-        constexpr int NM = X3 && h == 0 ? 2 : 1;
-        const uint4 bf = bq[u % RA];
-        if constexpr (u + RA < 2 * TP) bq[u % RA] = rdu(std::integral_constant<int, u + RA>{});
-#pragma unroll
-        for (int m = 0; m < NM; ++m)
-#pragma unroll
-          for (int i = 0; i < TC; ++i)
-            mfma_chunk<u16>(__builtin_bit_cast(uint4, wcur[i][X3 ? m : h]), bf, acc[i][j]);
-      });
-      __builtin_amdgcn_sched_group_barrier(0x100, RA, 0);
-      l1b_for<2 * TP>([&](auto uc) __attribute__((always_inline)) {
-        constexpr int u = decltype(uc)::value;
-        constexpr int NM = X3 && u / TP == 0 ? 2 : 1;
-        __builtin_amdgcn_sched_group_barrier(0x008, NM * TC, 0);
-        if constexpr (u + RA < 2 * TP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      });
-    }
+    half(std::integral_constant<int, 0>{});
+    half(std::integral_constant<int, 1>{});
   };
 
   auto epilogue = [&](int t) __attribute__((always_inline)) {
@@ -411,30 +380,12 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// SAD_V31_RA (A/B): 0 = per-half reads 4 ahead (round 3), else the rolling window
-static int v31_ra() {
-  static const int v = [] {
-    const char* e = getenv("SAD_V31_RA");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-template <int BC, bool POOL, bool X3, int RA>
-static int launch_halo256r_ra(const BlockConvArgs& a, hipStream_t s);
 template <int BC, bool POOL, bool X3>
 static int launch_halo256r_t(const BlockConvArgs& a, hipStream_t s) {
-  switch (v31_ra()) {
-    case 6: return launch_halo256r_ra<BC, POOL, X3, 6>(a, s);
-    case 8: return launch_halo256r_ra<BC, POOL, X3, 8>(a, s);
-    default: return launch_halo256r_ra<BC, POOL, X3, 0>(a, s);
-  }
-}
-template <int BC, bool POOL, bool X3, int RA>
-static int launch_halo256r_ra(const BlockConvArgs& a, hipStream_t s) {
   using namespace h31;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)halo256r_kernel<BC, POOL, X3, RA>,
+    (void)hipFuncSetAttribute((const void*)halo256r_kernel<BC, POOL, X3>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     attr = true;
   }
@@ -442,7 +393,7 @@ static int launch_halo256r_ra(const BlockConvArgs& a, hipStream_t s) {
   const int64_t tiles_p = (int64_t)a.N * (a.H / TH) * (a.W / TW);
   int64_t g = std::min<int64_t>(tiles_p * n_tc, 256);
   g = std::max<int64_t>(n_tc, g / n_tc * n_tc);
-  hipLaunchKernelGGL((halo256r_kernel<BC, POOL, X3, RA>), dim3((unsigned)g), dim3(512), SMEM, s, a);
+  hipLaunchKernelGGL((halo256r_kernel<BC, POOL, X3>), dim3((unsigned)g), dim3(512), SMEM, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }
