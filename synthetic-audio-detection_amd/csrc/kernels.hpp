@@ -91,7 +91,7 @@ struct L1BlockArgs {
   int w2_ld;
   const float* b2;
   int64_t x_bytes;       // set by launch_l1block
-  int ablate;            // reserved (0)
+  int ablate;            // timing ablations (wrong results): 1 no patch DMA, 2 no intermediate stores, 4 no output stores
   uint64_t* stamps;      // diagnostic builds only (-DSAD_STAMPS): s_memtime per tile phase
 };
 int launch_l1block(const L1BlockArgs& a, hipStream_t s);
