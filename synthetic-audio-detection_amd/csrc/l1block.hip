@@ -111,6 +111,9 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
   const int cg = wave & 1, pg = wave >> 1;
+  // timing ablations (wrong results; tools/l1bench.py --ablate): 1 no next-tile
+  // patch DMA, 2 no intermediate stores, 4 no output stores
+  const int ab = a.ablate;
   const int cw = cg * 32;  // this wave's first channel (both convs)
   const int w = xcd_remap(blockIdx.x, gridDim.x);
   const int tiles_y = a.H / 16, tiles_img = (a.W / 16) * tiles_y;
@@ -304,7 +307,7 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
         uint2 q;
         q.x = e1_qx;
         q.y = l1b_relu2(l1b_pk(acc[i][k][2], acc[i][k][3])) & e1_inm;
-        *(uint2*)(smem + (i ? e1_addr1 : e1_addr)) = q;
+        if (!(ab & 2)) *(uint2*)(smem + (i ? e1_addr1 : e1_addr)) = q;
       }
     };
     if (cont) {
@@ -384,7 +387,7 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
       const uint4 bf = bq[u % DQ];
       if constexpr (u + DQ < NU1) bq[u % DQ] = rd1(std::integral_constant<int, u + DQ>{});
       if constexpr (u % 5 == 0 && u / 5 < QP)
-        issue_piece(u / 5, onext, pb ^ 1, next_cont);
+        if (!(ab & 1)) issue_piece(u / 5, onext, pb ^ 1, next_cont);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         if constexpr (s == 0)
@@ -480,7 +483,8 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
         uint2 q;
         q.x = e2_qx;
         q.y = l1b_relu2(l1b_pk(acc2[i][jj][2], acc2[i][jj][3]));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(l1b_v2, q), ro,
+        if (!(ab & 4))
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(l1b_v2, q), ro,
                                               (jj * a.W + fr2) * 128 + (cw + 16 * i + 4 * fg2) * 2, obase, 0);
       }
     };
