@@ -899,9 +899,9 @@ extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_
   // plain conv launches, then bn_reduce over the stored output.
   const int64_t es = dtype == SAD_F32 ? 4 : 2, lim = (1ll << 31) - 65536;
   const bool one_launch = N * H * W * Cin * es < lim && a.M * Cout * es < lim;
-  // the patch-resident kernels (30, 31, 32) sum no statistics; their
+  // the patch-resident kernels (30, 31, 32, 43) sum no statistics; their
   // implicit-GEMM counterparts (13 / 15) do
-  if ((v == 30 || v == 31 || v == 32) && dtype == SAD_BF16 && one_launch) v = gemm_block_variant(a);
+  if ((v == 30 || v == 31 || v == 32 || v == 43) && dtype == SAD_BF16 && one_launch) v = gemm_block_variant(a);
   if (v == 41 && dtype == SAD_BF16 && one_launch) v = 20;  // variant 41 sums no statistics either
   const bool fused = dtype == SAD_BF16 && one_launch && (v == 13 || v == 15 || v == 20 || v == 25);
   int rows = 0;
