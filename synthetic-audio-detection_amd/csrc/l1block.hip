@@ -483,10 +483,7 @@ __global__ __launch_bounds__(256, 1) void l1block_kernel(L1BlockArgs a) {
         uint2 q;
         q.x = e2_qx;
         q.y = l1b_relu2(l1b_pk(acc2[i][jj][2], acc2[i][jj][3]));
-        if (ab & 256)  // SAD_L1_NT (A/B): non-temporal output stores
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(l1b_v2, q), ro,
-                                                (jj * a.W + fr2) * 128 + (cw + 16 * i + 4 * fg2) * 2, obase, 2);
-        else if (!(ab & 4))
+        if (!(ab & 4))
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(l1b_v2, q), ro,
                                                 (jj * a.W + fr2) * 128 + (cw + 16 * i + 4 * fg2) * 2, obase, 0);
       }
@@ -575,13 +572,8 @@ int launch_l1block(const L1BlockArgs& a_in, hipStream_t s) {
   // batch past that range into image ranges (every image is independent)
   const int64_t img = (int64_t)a_in.H * a_in.W * 128;
   const int64_t per = std::max<int64_t>(1, ((1ll << 31) - 65536) / img);
-  static const int nt = [] {
-    const char* e = getenv("SAD_L1_NT");
-    return e && atoi(e) ? 256 : 0;
-  }();
   for (int64_t n0 = 0; n0 < a_in.N; n0 += per) {
     L1BlockArgs a = a_in;
-    a.ablate |= nt;
     a.N = (int)std::min<int64_t>(per, a_in.N - n0);
     a.x = a_in.x + n0 * img / 2;
     a.out = a_in.out + n0 * img / 2;

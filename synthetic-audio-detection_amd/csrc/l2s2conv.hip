@@ -252,10 +252,7 @@ __global__ __launch_bounds__(256, 1) void l2s2conv_kernel(BlockConvArgs a) {
           }
           const int px = (8 * h + j + (fgt & 1)) * a.Wo + frt;
           const int co = cw + 16 * i + (fgt >> 1) * 8;
-          if (ab & 256)  // SAD_L2S2_NT (A/B): non-temporal output stores
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(l1b_v4, make_uint4(q[0], q[1], q[2], q[3])),
-                                                   ro, px * (int)(a.out_pstride * 2) + co * 2, obase, 2);
-          else if (!(ab & 8))
+          if (!(ab & 8))
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(l1b_v4, make_uint4(q[0], q[1], q[2], q[3])),
                                                    ro, px * (int)(a.out_pstride * 2) + co * 2, obase, 0);
           const f32x4 b0 = biasv(i);
@@ -284,11 +281,6 @@ int launch_l2s2conv(const BlockConvArgs& a, hipStream_t s) {
   const int64_t g = std::min<int64_t>(tiles, 256);
   BlockConvArgs b = a;
   b.out_bytes = ((int64_t)a.N * a.Ho * a.Wo - 1) * a.out_pstride * 2 + 256;
-  static const int nt = [] {
-    const char* e = getenv("SAD_L2S2_NT");
-    return e && atoi(e) ? 256 : 0;
-  }();
-  b.ablate |= nt;
   SAD_REQUIRE(b.out_bytes < (1ll << 31) - 65536, "variant 43: output passes the 32-bit buffer range");
   static bool attr = false;
   if (!attr) {
