@@ -19,6 +19,7 @@
 //   float64 mean / unbiased variance -> standardise (32,128 values).
 #include <math.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "common.hpp"
@@ -42,6 +43,13 @@ struct FrontendPlan {
   int* d_mel_len = nullptr;    // [n_mels]
   int* d_mel_off = nullptr;    // [n_mels] offset into d_mel_w
   float* d_mel_w = nullptr;    // packed nonzero weights
+  // staged mel projection by lane (n_mels <= FE_STAGE_MELS): lane l sums mel
+  // rows lane_tab[l] (q = 0) and lane_tab[64 + l] (q = 1; -1: none) from bins
+  // bin_lo + lane_tab[128 + q * 64 + l] .. + ml[q] - 1, weights [ml0 + ml1][64]
+  // zero past the row's filter (null: the CSR loop)
+  int* d_lane_tab = nullptr;
+  float* d_lane_w = nullptr;
+  int ml0 = 0, ml1 = 0;
   int device = 0;
 };
 
@@ -96,9 +104,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 constexpr int FE_STAGE_MELS = 128;  // dB rows staged in LDS for coalesced stores
 constexpr int FE_POW = 800;         // power bins per wave in LDS (the reference's bank: 767)
 constexpr int FE_ZBUF = FE_NC + 16;  // spectrum slots per wave (fe_zslot padding)
-constexpr int FE_MAX_NNZ = 1600;    // mel weights in LDS (1515 for the reference's bank)
-// LDS: twiddles 8 KB + 4 FFT buffers 32.5 KB + power 12.5 KB + dB staging 16.5 KB +
-// mel weights 6.3 KB = 76 KB: two workgroups per CU.
+// LDS: twiddles 8 KB + 4 FFT buffers 32.5 KB + power 12.5 KB + dB staging 16.5 KB
+// = 70 KB: two workgroups per CU.  (The mel weights are read from the lane
+// table in global memory, L1-resident: 11.5 KB for the reference's bank.)
 
 template <typename IT>  // int16_t PCM (scaled by 1/32768, torchaudio.load normalize) or float
 __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
@@ -107,13 +115,13 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     int n_frames, int hop,
     const float2* __restrict__ tw1024, const float* __restrict__ window, const int* __restrict__ mel_start,
     const int* __restrict__ mel_len, const int* __restrict__ mel_off, const float* __restrict__ mel_w, int nnz,
-    int n_mels, int bin_lo, int bin_hi, float* __restrict__ out) {
+    int n_mels, int bin_lo, int bin_hi, const int* __restrict__ lane_tab, const float* __restrict__ lane_w, int ml0,
+    int ml1, float* __restrict__ out) {
   __shared__ float2 s_tw[FE_NC];
   __shared__ float2 s_buf[FE_WAVES][FE_ZBUF];
   __shared__ float2 s_tw3[64];  // W64^{q k2} at [k2][q]
   __shared__ float s_pow[FE_WAVES][FE_POW];
   __shared__ float s_db[FE_STAGE_MELS][FE_FRAMES_PER_WG + 1];
-  __shared__ float s_melw[FE_MAX_NNZ];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t seg = blockIdx.y;
@@ -127,21 +135,22 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
   }
   const IT* x = pcm + x0;
   const float in_scale = sizeof(IT) == 2 ? (1.0f / 32768.0f) : 1.0f;
-  const bool staged = n_mels <= FE_STAGE_MELS && bin_hi - bin_lo < FE_POW && nnz <= FE_MAX_NNZ;
+  // staged: the mel rows by lane table (plan_create builds it when n_mels <=
+  // FE_STAGE_MELS and the padded rows fit the power buffer), dB rows through LDS
+  const bool staged = lane_w != nullptr;
   for (int i = tid; i < FE_NC; i += 256) s_tw[i] = tw1024[i];
-  if (staged)
-    for (int i = tid; i < nnz; i += 256) s_melw[i] = mel_w[i];
-  // this lane's mel rows (staged path): m = lane and n_mels-1-lane -- filters
-  // widen with m, so the pair's lengths sum to about the same for every lane
-  int mm[2], mk0[2], mlen[2], moff[2];
+  // this lane's mel rows (staged path) from the lane table: mm = the row (-1:
+  // none), mk0 = its first bin - bin_lo; the power buffer's tail past bin_hi is
+  // read (times a zero weight) by the padded rows: zero it once, the frames
+  // never write it
+  int mm[2] = {-1, -1}, mk0[2] = {0, 0};
+  if (staged) {
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int m = q == 0 ? lane : n_mels - 1 - lane;
-    const bool ok = q == 0 ? lane < n_mels : m >= 64;
-    mm[q] = ok ? m : -1;
-    mk0[q] = ok ? mel_start[m] : 0;
-    mlen[q] = ok ? mel_len[m] : 0;
-    moff[q] = ok ? mel_off[m] : 0;
+    for (int q = 0; q < 2; ++q) {
+      mm[q] = lane_tab[q * 64 + lane];
+      mk0[q] = lane_tab[128 + q * 64 + lane];
+    }
+    for (int i = bin_hi - bin_lo + 1 + lane; i < FE_POW; i += 64) s_pow[wave][i] = 0.f;
   }
   __syncthreads();
 
@@ -283,16 +292,21 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     }
     wave_lds_sync();
     if (staged) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (mm[q] >= 0) {
-          const float* pp = pw + mk0[q] - bin_lo;
-          const float* ww = s_melw + moff[q];
-          float acc = 0.f;
-          for (int i = 0; i < mlen[q]; ++i) acc = fmaf(pp[i], ww[i], acc);
-          s_db[mm[q]][t - f_begin] = 10.0f * log10f(fmaxf(acc, 1e-10f));
-        }
-      }
+      // every lane runs ml0 + ml1 steps (no divergence, independent loads):
+      // the row's bins in order, then zero weights -- the same sums as the
+      // CSR loop, bit for bit; the rows are spread over the lanes so their
+      // start bins rarely share an LDS bank (plan_create)
+      const float* pa = pw + mk0[0];
+      const float* pb = pw + mk0[1];
+      const float* wa = lane_w + lane;
+      const float* wb = lane_w + ml0 * 64 + lane;
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll 4
+      for (int i = 0; i < ml0; ++i) a0 = fmaf(pa[i], wa[i * 64], a0);
+#pragma unroll 4
+      for (int i = 0; i < ml1; ++i) a1 = fmaf(pb[i], wb[i * 64], a1);
+      if (mm[0] >= 0) s_db[mm[0]][t - f_begin] = 10.0f * log10f(fmaxf(a0, 1e-10f));
+      if (mm[1] >= 0) s_db[mm[1]][t - f_begin] = 10.0f * log10f(fmaxf(a1, 1e-10f));
     } else {
       for (int m = lane; m < n_mels; m += 64) {
         const int k0 = mel_start[m], len = mel_len[m], off = mel_off[m];
@@ -498,6 +512,55 @@ extern "C" int sad_frontend_plan_create(const sad_frontend_cfg* cfg, sad_fronten
   p->bin_lo = lo;
   p->bin_hi = hi;
   p->nnz = (int)w.size();
+  // lane table of the staged mel projection: the shorter half of the rows on
+  // q = 0, the longer on q = 1 (each padded to its longest row); within each,
+  // rows longest first into the 32-lane half (ds_read_b32 bank group) holding
+  // fewer rows whose start bin falls on the same bank
+  std::vector<int> lane_tab(256, 0);
+  std::vector<float> lane_w;
+  bool lanes_ok = cfg->n_mels <= FE_STAGE_MELS && hi - lo < FE_POW;
+  if (lanes_ok) {
+    std::vector<int> ord(cfg->n_mels);
+    for (int m = 0; m < cfg->n_mels; ++m) ord[m] = m;
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return ln[x] < ln[y]; });
+    const int nA = std::min(cfg->n_mels, 64);
+    int ml[2] = {0, 0};
+    for (int q = 0; q < 2; ++q) {
+      std::vector<int> rows(q == 0 ? ord.begin() : ord.begin() + nA, q == 0 ? ord.begin() + nA : ord.end());
+      std::stable_sort(rows.begin(), rows.end(), [&](int x, int y) { return ln[x] > ln[y]; });
+      std::vector<int> grp[2];
+      for (int m : rows) {
+        int best = -1, bc = 1 << 30;
+        for (int g = 0; g < 2; ++g) {
+          if ((int)grp[g].size() >= 32) continue;
+          int c = 0;
+          for (int x : grp[g]) c += ((st[x] - lo) % 32 == (st[m] - lo) % 32) && st[x] != st[m];
+          if (c < bc) bc = c, best = g;
+        }
+        grp[best].push_back(m);
+      }
+      for (int l = 0; l < 64; ++l) {
+        const int g = l >> 5, k = l & 31;
+        const int m = k < (int)grp[g].size() ? grp[g][k] : -1;
+        lane_tab[q * 64 + l] = m;
+        lane_tab[128 + q * 64 + l] = m >= 0 ? st[m] - lo : 0;
+        if (m >= 0) ml[q] = std::max(ml[q], ln[m]);
+      }
+    }
+    for (int q = 0; q < 2 && lanes_ok; ++q)
+      for (int l = 0; l < 64; ++l) lanes_ok = lanes_ok && lane_tab[128 + q * 64 + l] + ml[q] <= FE_POW;
+    if (lanes_ok) {
+      lane_w.assign((size_t)(ml[0] + ml[1]) * 64, 0.f);
+      for (int q = 0; q < 2; ++q)
+        for (int l = 0; l < 64; ++l) {
+          const int m = lane_tab[q * 64 + l];
+          if (m < 0) continue;
+          for (int i = 0; i < ln[m]; ++i) lane_w[(size_t)((q ? ml[0] : 0) + i) * 64 + l] = w[off[m] + i];
+        }
+      p->ml0 = ml[0];
+      p->ml1 = ml[1];
+    }
+  }
   std::vector<float2> tw(FE_NC), tw2(FE_NC + 1);
   for (int m = 0; m < FE_NC; ++m) {
     const double a = -2.0 * M_PI * m / FE_NC;
@@ -519,6 +582,10 @@ extern "C" int sad_frontend_plan_create(const sad_frontend_cfg* cfg, sad_fronten
   UP(p->d_mel_len, ln);
   UP(p->d_mel_off, off);
   UP(p->d_mel_w, w);
+  if (lanes_ok) {
+    UP(p->d_lane_tab, lane_tab);
+    UP(p->d_lane_w, lane_w);
+  }
 #undef UP
   *out = p;
   return SAD_OK;
@@ -533,6 +600,8 @@ extern "C" int sad_frontend_plan_destroy(sad_frontend_plan* p) {
   (void)hipFree(p->d_mel_len);
   (void)hipFree(p->d_mel_off);
   (void)hipFree(p->d_mel_w);
+  if (p->d_lane_tab) (void)hipFree(p->d_lane_tab);
+  if (p->d_lane_w) (void)hipFree(p->d_lane_w);
   delete p;
   return SAD_OK;
 }
@@ -564,7 +633,7 @@ static int frontend_run(const sad_frontend_plan* p, const IT* pcm, int64_t n_seg
                        seg_offs ? pcm : pcm + done * seg_stride, seg_stride, seg_offs ? seg_offs + done : nullptr,
                        max_off, p->cfg.n_samples, p->n_frames, p->cfg.hop_length, p->d_tw1024, p->d_window,
                        p->d_mel_start, p->d_mel_len, p->d_mel_off, p->d_mel_w, p->nnz, p->cfg.n_mels, p->bin_lo,
-                       p->bin_hi, dbbuf + off);
+                       p->bin_hi, p->d_lane_tab, p->d_lane_w, p->ml0, p->ml1, dbbuf + off);
     SAD_CHECK_HIP(hipGetLastError());
     hipLaunchKernelGGL(fe_normalize_kernel, dim3((unsigned)chunk), dim3(1024), 0, s, dbbuf + off,
                        p->cfg.n_mels * p->n_frames, p->cfg.top_db, out_map + off);
