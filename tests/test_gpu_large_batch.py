@@ -67,3 +67,22 @@ def test_backbone_micro_batch_1024_equals_512():
     _, m512 = Engine(sd, DEV, dtype='bf16', micro_batch=512).forward_pcm(pcm)
     torch.cuda.synchronize()
     assert torch.equal(m1024, m512)
+
+
+def test_backbone_micro_batch_2048_equals_1024():
+    """The bench's micro-batch (2,048 segments: layer1's output is 4 GiB, so
+    every layer2 conv runs as image-range launches) against two 1,024-segment
+    micro-batches, bit for bit."""
+    import os
+
+    from conftest import GOLDEN
+    from sad import _lib, weights as sw
+    from sad.engine import Engine
+    sd = sw.merged_state_dict(0, 6, False, bn_stats=sw.load_bn_stats(os.path.join(GOLDEN, 'bn_stats_n6.npz')))
+    B = 2048
+    pcm = torch.empty(B, 128000, dtype=torch.int16, device=DEV)
+    _lib.call('sad_synth_pcm', 11, 0, B, 128000, _lib.ptr(pcm), _lib.stream_handle(torch.device(DEV)))
+    _, m2048 = Engine(sd, DEV, dtype='bf16', micro_batch=2048).forward_pcm(pcm)
+    _, m1024 = Engine(sd, DEV, dtype='bf16', micro_batch=1024).forward_pcm(pcm)
+    torch.cuda.synchronize()
+    assert torch.equal(m2048, m1024)
