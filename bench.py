@@ -202,9 +202,13 @@ def ingest_leg(eng, dev, minutes: float = 2.0, reps: int = 3):
 
 
 class Mode:
-    """One engine configuration timed on this rank's resident PCM."""
+    """One engine configuration timed on this rank's resident PCM.
 
-    def __init__(self, sd, dev, dtype, micro_batch, B, world):
+    overlap: the next step's front end runs on a side stream while this step's
+    backbone runs (two map buffers; each step still computes its whole batch
+    through every stage, the front end just starts one step early)."""
+
+    def __init__(self, sd, dev, dtype, micro_batch, B, world, overlap=False):
         from sad.engine import Engine
         self.eng = Engine(sd, dev, dtype=dtype, micro_batch=micro_batch)
         self.dtype, self.mb, self.B, self.world, self.dev = dtype, micro_batch, B, world, dev
@@ -212,14 +216,45 @@ class Mode:
         self.logits = torch.empty(B, HEADS, 2, device=dev)
         self.merged = torch.empty(B, HEADS + 1, device=dev)
         self.gathered = torch.empty(world * B, HEADS + 1, device=dev) if world > 1 else None
+        self.overlap = overlap
+        if overlap:
+            self.side = torch.cuda.Stream(dev)
+            self.maps = [None, None]
+            self.fe_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self.bb_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self.i = 0
+            self.fe_ev = [None, None]  # the events timing the front end that filled each slot
+
+    def _frontend_ahead(self, pcm, slot, ev=None):
+        # the slot's previous reader (the backbone two steps back) must be done
+        self.side.wait_event(self.bb_done[slot])
+        if ev is not None:
+            ev[0].record(self.side)
+        with torch.cuda.stream(self.side):
+            self.maps[slot] = self.eng.frontend(pcm, out=self.maps[slot])
+        if ev is not None:
+            ev[1].record(self.side)
+        self.fe_done[slot].record(self.side)
 
     def step(self, pcm, ev=None):
+        if self.overlap:
+            slot = self.i & 1
+            if self.i == 0:
+                self._frontend_ahead(pcm, slot)
+            cur = torch.cuda.current_stream()
+            cur.wait_event(self.fe_done[slot])
+            m = self.maps[slot]
+        else:
+            if ev is not None:
+                ev[0].record()
+            m = self.eng.frontend(pcm)
+            if ev is not None:
+                ev[1].record()
         if ev is not None:
-            ev[0].record()
-        m = self.eng.frontend(pcm)
-        if ev is not None:
-            ev[1].record()
+            ev[5].record()
         self.eng.backbones[0](m, out=self.feats)
+        if self.overlap:
+            self.bb_done[slot].record(cur)
         if ev is not None:
             ev[2].record()
         self.eng.heads([self.feats], self.logits, self.merged)
@@ -232,6 +267,10 @@ class Mode:
                 dist.all_gather(list(self.gathered.chunk(self.world)), self.merged)
         if ev is not None:
             ev[4].record()
+        if self.overlap:
+            # the next step's front end (its events time it on the side stream)
+            self._frontend_ahead(pcm, slot ^ 1, ev)
+            self.i += 1
 
     def run(self, pcm, steps, warmup, profile=True):
         from sad import _lib
@@ -241,7 +280,7 @@ class Mode:
         if self.world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(steps)]
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
         t0 = time.perf_counter()
         for i in range(steps):
             if profile and i == steps - 1:
@@ -258,7 +297,7 @@ class Mode:
         _lib.call('sad_profile_end', DOMINANT_VARIANT[self.dtype] if profile else -1, _lib.ctypes.byref(k_ms),
                   _lib.ctypes.byref(k_n), _lib.ctypes.byref(k_fl))
         mean = lambda a, b: sum(e[a].elapsed_time(e[b]) for e in evs) / steps  # noqa: E731
-        r = {'elapsed': elapsed, 'fe_ms': mean(0, 1), 'bb_ms': mean(1, 2), 'heads_ms': mean(2, 3),
+        r = {'elapsed': elapsed, 'fe_ms': mean(0, 1), 'bb_ms': mean(5, 2), 'heads_ms': mean(2, 3),
              'gather_ms': mean(3, 4), 'k_ms': k_ms.value, 'k_n': k_n.value, 'k_flop': k_fl.value}
         r['rank_ms_per_step'] = [round(elapsed * 1e3 / steps, 3)]
         r['rank_gather_ms'] = [round(r['gather_ms'], 4)]
@@ -303,6 +342,9 @@ def main():
     ap.add_argument('--parity-steps', type=int, default=0, help='timed steps of the bf16x3 parity mode '
                                                                 '(0: max(steps // 3, 3); -1: skip)')
     ap.add_argument('--fp32-steps', type=int, default=2, help='timed steps of the fp32 mode (N = 1; 0: skip)')
+    ap.add_argument('--overlap-frontend', type=int, default=0,
+                    help='1: each step\'s front end runs on a side stream during the previous step\'s backbone '
+                         '(headline mode only)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--kernels-only', action='store_true',
                     help='profiling runs: only the headline mode (no parity/fp32 legs, accuracy or CPU baseline)')
@@ -331,7 +373,7 @@ def main():
     pcm = torch.empty(B, SEG, dtype=torch.int16, device=dev)
     _lib.call('sad_synth_pcm', 0, rank * B, B, SEG, _lib.ptr(pcm), _lib.stream_handle(dev))
 
-    head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world)
+    head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world, overlap=bool(args.overlap_frontend))
     r = head.run(pcm, args.steps, args.warmup)
     p_steps = max(args.steps // 3, 3) if args.parity_steps == 0 else args.parity_steps
     if args.kernels_only:
@@ -387,7 +429,7 @@ def main():
             'config': {'workload': 'end-to-end inference: B int16 4 s segments resident in HBM -> mel front end '
                                    '-> ResNet-18@512x512 -> 6 binary heads -> merge (+RCCL all-gather of logits)',
                        'segments_per_gpu_per_step': B, 'heads': HEADS, 'distinct_backbones': 1,
-                       'micro_batch': head.mb, 'parallelism': f'dp{world}',
+                       'micro_batch': head.mb, 'frontend_overlap': head.overlap, 'parallelism': f'dp{world}',
                        'per_rank_ms_per_step': r['rank_ms_per_step'], 'per_rank_allgather_ms': r['rank_gather_ms']},
             'roofline': {'bound': 'mfma',
                          'kernel': DOMINANT_DESC,
