@@ -236,7 +236,10 @@ class Mode:
             ev[1].record(self.side)
         self.fe_done[slot].record(self.side)
 
-    def step(self, pcm, ev=None):
+    def step(self, pcm, ev=None, next_pcm=None):
+        # (overlap: pcm is this step's batch -- its maps were computed during
+        # the previous step, except for the first -- and next_pcm the next
+        # step's, whose front end starts now; the bench repeats one batch)
         if self.overlap:
             slot = self.i & 1
             if self.i == 0:
@@ -269,8 +272,27 @@ class Mode:
             ev[4].record()
         if self.overlap:
             # the next step's front end (its events time it on the side stream)
-            self._frontend_ahead(pcm, slot ^ 1, ev)
+            self._frontend_ahead(pcm if next_pcm is None else next_pcm, slot ^ 1, ev)
             self.i += 1
+
+    def isolated(self, pcm, reps=5):
+        """Front end and backbone timed alone (sequentially, HIP events on the
+        current stream): the per-stage rooflines of an overlapped run, whose
+        concurrent stages stretch each other."""
+        cur = torch.cuda.current_stream()
+        torch.cuda.synchronize()
+        fe, bb = [], []
+        for _ in range(reps):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record(cur)
+            m = self.eng.frontend(pcm)
+            e[1].record(cur)
+            self.eng.backbones[0](m, out=self.feats)
+            e[2].record(cur)
+            torch.cuda.synchronize()
+            fe.append(e[0].elapsed_time(e[1]))
+            bb.append(e[1].elapsed_time(e[2]))
+        return sorted(fe)[reps // 2], sorted(bb)[reps // 2]
 
     def run(self, pcm, steps, warmup, profile=True):
         from sad import _lib
@@ -342,7 +364,7 @@ def main():
     ap.add_argument('--parity-steps', type=int, default=0, help='timed steps of the bf16x3 parity mode '
                                                                 '(0: max(steps // 3, 3); -1: skip)')
     ap.add_argument('--fp32-steps', type=int, default=2, help='timed steps of the fp32 mode (N = 1; 0: skip)')
-    ap.add_argument('--overlap-frontend', type=int, default=0,
+    ap.add_argument('--overlap-frontend', type=int, default=1,
                     help='1: each step\'s front end runs on a side stream during the previous step\'s backbone '
                          '(headline mode only)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -375,6 +397,11 @@ def main():
 
     head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world, overlap=bool(args.overlap_frontend))
     r = head.run(pcm, args.steps, args.warmup)
+    if head.overlap:
+        # the stage rooflines from the stages run alone (overlapped, the side
+        # stream's front end and the backbone stretch each other)
+        r['fe_ms_overlapped'], r['bb_ms_overlapped'] = r['fe_ms'], r['bb_ms']
+        r['fe_ms'], r['bb_ms'] = head.isolated(pcm)
     p_steps = max(args.steps // 3, 3) if args.parity_steps == 0 else args.parity_steps
     if args.kernels_only:
         p_steps, args.fp32_steps, args.no_cpu_baseline = -1, 0, True
@@ -441,7 +468,9 @@ def main():
                          'backbone': {'achieved': round(bb_alg * fac, 1), 'frac': round(bb_alg * fac / peak, 4),
                                       'ms_per_step': round(r['bb_ms'], 3), 'flop_per_segment': BACKBONE_FLOP,
                                       'what': 'fused resize+stem + 16 block-conv GEMMs + avgpool, HIP events '
-                                              'around the backbone call'},
+                                              'around the backbone call' + (' (run alone after the timed steps; '
+                                              f'overlapped with the next front end: {r["bb_ms_overlapped"]:.3f} ms)'
+                                              if head.overlap else '')},
                          'measured_gemm_ceiling_tflops': 1344.0,
                          # front end (configs[1]): fused STFT/mel/dB + standardise, fp32 VALU-bound
                          # (16.4 MFLOP and 384,512 B per segment)
@@ -450,7 +479,11 @@ def main():
                                       'peak_tflops': F32_PEAK_TFLOPS,
                                       'frac': round(FE_FLOP * B / (r['fe_ms'] * 1e-3) / 1e12 / F32_PEAK_TFLOPS, 4),
                                       'achieved_gbps': round(FE_BYTES * B / (r['fe_ms'] * 1e-3) / 1e9, 1),
-                                      'segments_per_s': round(B / (r['fe_ms'] * 1e-3), 1)}},
+                                      'segments_per_s': round(B / (r['fe_ms'] * 1e-3), 1),
+                                      **({'overlapped_ms_per_step': round(r['fe_ms_overlapped'], 3),
+                                          'what': 'timed alone after the timed steps; in them it runs on a side '
+                                                  'stream during the previous step\'s backbone'}
+                                         if head.overlap else {})}},
             'accuracy': accuracy(head),
         }
         if par is not None:
