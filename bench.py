@@ -366,7 +366,7 @@ def main():
     ap.add_argument('--fp32-steps', type=int, default=2, help='timed steps of the fp32 mode (N = 1; 0: skip)')
     ap.add_argument('--overlap-frontend', type=int, default=1,
                     help='1: each step\'s front end runs on a side stream during the previous step\'s backbone '
-                         '(headline mode only)')
+                         '(the headline and parity modes)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--kernels-only', action='store_true',
                     help='profiling runs: only the headline mode (no parity/fp32 legs, accuracy or CPU baseline)')
@@ -410,8 +410,10 @@ def main():
         if args.dtype == 'bf16x3':
             par_mode, par = head, r
         else:
-            par_mode = Mode(sd, dev, 'bf16x3', mbs['bf16x3'], B, world)
+            par_mode = Mode(sd, dev, 'bf16x3', mbs['bf16x3'], B, world, overlap=bool(args.overlap_frontend))
             par = par_mode.run(pcm, p_steps, 1)
+            if par_mode.overlap:
+                par['fe_ms'], par['bb_ms'] = par_mode.isolated(pcm, reps=3)
 
     if rank == 0:
         from sad.engine import Engine
