@@ -251,7 +251,8 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
         if constexpr (u + DQ < NUC) bq[u % DQ] = rd(std::integral_constant<int, u + DQ>{});
         // DMA: chunk 0 carries this tile's chunk-1 patch and residual; chunk 1
         // the next tile's chunk-0 patch
-        if constexpr (u % PDIV == 0 && u / PDIV < QP) issue_piece(u / PDIV, c == 0 ? o : onext, c ^ 1);
+        if constexpr (u % PDIV == 0 && u / PDIV < QP)
+          if (!(a.ablate & 32)) issue_piece(u / PDIV, c == 0 ? o : onext, c ^ 1);
         if constexpr (RES && c == 0 && u % PDIV == PDIV / 2 && u / PDIV < NRP) issue_res(u / PDIV, o);
         if constexpr (DS && c == 0 && u % 32 == 8 && u / 32 < NDS) issue_ds(u / 32, o);
         auto mm = [&](auto ic, auto sc) __attribute__((always_inline)) {
@@ -425,7 +426,8 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
         }
         const int px = (j + (fgt & 1)) * a.W + frt;
         const int co = cw + 16 * i + (fgt >> 1) * 8;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(l1b_v4, make_uint4(q[0], q[1], q[2], q[3])), ro,
+        if (!(a.ablate & 8))  // timing ablations (wrong results): 8 no output stores, 32 no patch DMA
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(l1b_v4, make_uint4(q[0], q[1], q[2], q[3])), ro,
                                                px * (int)(a.out_pstride * 2) + co * 2, obase, 0);
         const f32x4 b0 = biasv(i);
         acc[i][j] = b0;
