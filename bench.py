@@ -29,7 +29,11 @@ import argparse
 import json
 import os
 import platform
+import re
+import statistics
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -47,20 +51,69 @@ BACKBONE_FLOP = 18.13e9        # ResNet-18 @512^2 with conv1's 3 identical chann
 BF16_PEAK_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3        # f32 MFMA = f32 vector peak (MI355X_MICROARCH.md)
 # The dominant kernel and its rocprof key in the committed PMC traffic file
-# bf16: variant 31 (csrc/halo256r.hip), the 12 stride-1 layer3/4 convs of a
+# bf16: variant 31 (csrc/halo256r.hip), the stride-1 layer3/4 convs of a
 # 2,048-segment step; the split-bf16 parity mode runs its split form on the same convs
 DOMINANT_VARIANT = {'bf16': 31, 'bf16x3': 31, 'fp32': 13}
 # rocprof names the kernel with its template arguments ('sad::halo256r_kernel<256, false>|131072'); the
 # key is resolved by this name prefix (see dominant_traffic), so a template change cannot make it stale
 DOMINANT_KERNEL_PREFIX = 'sad::halo256r_kernel<'
 DOMINANT_DESC = ('sad::halo256r_kernel (variant 31): patch-resident 256-channel x 16x16-pixel conv, weights '
-                 'streamed into registers; the 12 stride-1 layer3/4 convs of a step (stride-2 convs stay on the '
-                 '256x256 implicit GEMM, variant 13)')
+                 'streamed into registers; the stride-1 layer3/4 convs of a step (5 convs; layer3.0 conv2 + downsample '
+                 'runs as two image-range launches at micro-batch 2,048, the last one fuses the average pool; the '
+                 'stride-2 convs stay on the 256x256 implicit GEMM, variant 13)')
 TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r04_pmc_traffic.json', 'r03_pmc_traffic.json')
                      if os.path.exists(os.path.join(ROOT, 'profiles', f))), '')
 FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats
 FE_BYTES = 256000 + 128512     # int16 PCM read + fp32 [128, 251] map written
 HEADS = 6
+
+
+class ClockSampler:
+    """Shader clock and package power from `rocm-smi` (a daemon thread) while
+    the timed steps run.  The board holds a power-limited clock in this loop
+    ('The power cap'), so the dense MFMA peak at that clock is
+    the ceiling the kernels face; `roofline.clock` reports it next to the
+    2.4 GHz `peak`.  Best effort: no rocm-smi, no samples -> None."""
+
+    def __init__(self, local_rank: int):
+        vis = os.environ.get('ROCR_VISIBLE_DEVICES') or os.environ.get('HIP_VISIBLE_DEVICES') or ''
+        ids = [v for v in vis.split(',') if v.strip().isdigit()]
+        self.gpu = int(ids[local_rank]) if local_rank < len(ids) else local_rank
+        self.samples, self._stop, self._th = [], threading.Event(), None
+
+    def _loop(self):
+        while not self._stop.is_set():
+            try:
+                txt = subprocess.run(['rocm-smi', '--showclocks', '--showpower'], capture_output=True, text=True,
+                                     timeout=10).stdout
+            except Exception:
+                return
+            sclk, power = {}, {}
+            for line in txt.splitlines():
+                m = re.match(r'GPU\[(\d+)\].*sclk clock level: \S+ \((\d+)Mhz\)', line)
+                if m:
+                    sclk[int(m.group(1))] = int(m.group(2))
+                m = re.match(r'GPU\[(\d+)\].*Graphics Package Power \(W\): ([\d.]+)', line)
+                if m:
+                    power[int(m.group(1))] = float(m.group(2))
+            g = self.gpu if self.gpu in sclk else (min(sclk) if sclk else None)
+            if g is not None:
+                self.samples.append((sclk[g], power.get(g)))
+            self._stop.wait(0.1)
+
+    def start(self):
+        self._th = threading.Thread(target=self._loop, daemon=True)
+        self._th.start()
+
+    def stop(self):
+        self._stop.set()
+        if self._th is not None:
+            self._th.join(timeout=12)
+        if not self.samples:
+            return None
+        pw = [p for _, p in self.samples if p is not None]
+        return {'sclk_mhz_median': statistics.median(s for s, _ in self.samples),
+                'power_w_median': statistics.median(pw) if pw else None, 'samples': len(self.samples)}
 
 
 def dominant_traffic(tr: dict, prefix: str = DOMINANT_KERNEL_PREFIX):
@@ -294,7 +347,7 @@ class Mode:
             bb.append(e[1].elapsed_time(e[2]))
         return sorted(fe)[reps // 2], sorted(bb)[reps // 2]
 
-    def run(self, pcm, steps, warmup, profile=True):
+    def run(self, pcm, steps, warmup, profile=True, clock=None):
         from sad import _lib
         for _ in range(warmup):
             self.step(pcm)
@@ -303,6 +356,8 @@ class Mode:
             dist.barrier()
         torch.cuda.synchronize()
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
+        if clock is not None:
+            clock.start()
         t0 = time.perf_counter()
         for i in range(steps):
             if profile and i == steps - 1:
@@ -315,12 +370,13 @@ class Mode:
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        clk = clock.stop() if clock is not None else None
         k_ms, k_n, k_fl = _lib.ctypes.c_double(), _lib.I64(), _lib.ctypes.c_double()
         _lib.call('sad_profile_end', DOMINANT_VARIANT[self.dtype] if profile else -1, _lib.ctypes.byref(k_ms),
                   _lib.ctypes.byref(k_n), _lib.ctypes.byref(k_fl))
         mean = lambda a, b: sum(e[a].elapsed_time(e[b]) for e in evs) / steps  # noqa: E731
         r = {'elapsed': elapsed, 'fe_ms': mean(0, 1), 'bb_ms': mean(5, 2), 'heads_ms': mean(2, 3),
-             'gather_ms': mean(3, 4), 'k_ms': k_ms.value, 'k_n': k_n.value, 'k_flop': k_fl.value}
+             'gather_ms': mean(3, 4), 'k_ms': k_ms.value, 'k_n': k_n.value, 'k_flop': k_fl.value, 'clock': clk}
         r['rank_ms_per_step'] = [round(elapsed * 1e3 / steps, 3)]
         r['rank_gather_ms'] = [round(r['gather_ms'], 4)]
         if self.world > 1:
@@ -342,6 +398,17 @@ def kernel_roofline(r, mfma_factor=1):
     alg = r['k_flop'] / (r['k_ms'] * 1e-3) / 1e12 if r['k_ms'] > 0 else 0.0
     return alg, alg * mfma_factor, {'launches': r['k_n'], 'launch_avg_us': round(r['k_ms'] * 1e3 / n, 2),
                                     'flop_per_launch': round(r['k_flop'] / n)}
+
+
+def held_clock(clk, achieved, peak, peak_mhz=2400.0):
+    """roofline.clock: the clock the board held during the timed steps and the
+    dominant kernel's fraction of the MFMA peak at that clock."""
+    if not clk:
+        return None
+    at = peak * clk['sclk_mhz_median'] / peak_mhz
+    return {**clk, 'peak_mhz': peak_mhz, 'peak_at_held_clock': round(at, 1),
+            'frac_at_held_clock': round(achieved / at, 4),
+            'source': 'rocm-smi --showclocks --showpower sampled during the timed steps (rank 0)'}
 
 
 def decisions(merged):
@@ -396,7 +463,8 @@ def main():
     _lib.call('sad_synth_pcm', 0, rank * B, B, SEG, _lib.ptr(pcm), _lib.stream_handle(dev))
 
     head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world, overlap=bool(args.overlap_frontend))
-    r = head.run(pcm, args.steps, args.warmup)
+    sample_clock = rank == 0 and os.environ.get('SAD_BENCH_CLOCK', '1') != '0'  # 0: no rocm-smi sampling (A/B)
+    r = head.run(pcm, args.steps, args.warmup, clock=ClockSampler(local) if sample_clock else None)
     if head.overlap:
         # the stage rooflines from the stages run alone (overlapped, the side
         # stream's front end and the backbone stretch each other)
@@ -474,6 +542,7 @@ def main():
                                               f'overlapped with the next front end: {r["bb_ms_overlapped"]:.3f} ms)'
                                               if head.overlap else '')},
                          'measured_gemm_ceiling_tflops': 1344.0,
+                         'clock': held_clock(r['clock'], exe, peak),
                          # front end (configs[1]): fused STFT/mel/dB + standardise, fp32 VALU-bound
                          # (16.4 MFLOP and 384,512 B per segment)
                          'frontend': {'ms_per_step': round(r['fe_ms'], 3),
