@@ -331,7 +331,7 @@ static int timed_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, do
 // SAD_L1_FUSED=0 runs layer1's blocks as two convs each (variant 25) instead of
 // the fused BasicBlock kernel (variant 40; A/B switch).  Same box, 2 rounds:
 // fused with 128-segment front sub-batches 52.5k seg/s vs 51.5k unfused at 32
-static bool l1_fused() {
+bool sad::l1_fused() {
   static const bool v = [] {
     const char* e = getenv("SAD_L1_FUSED");
     return e ? atoi(e) != 0 : true;

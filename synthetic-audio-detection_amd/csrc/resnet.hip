@@ -7,8 +7,11 @@
 // Launch plan per micro-batch (NHWC activations in the plan dtype):
 //   fused resize + stem (conv1 7x7/2 + bn1 + relu + maxpool)  -> X [128,128,64]
 //   BasicBlock:  T1 = relu(conv3x3/s(X))
-//                Y  = relu(conv3x3(T1) + shortcut)   one GEMM: the identity or
-//                     the folded 1x1/s downsample are extra K columns over X
+//                Y  = relu(conv3x3(T1) + shortcut)   the folded 1x1/s downsample
+//                     as extra K columns over X; the identity as an epilogue
+//                     residual where the halo / resident-weight kernels run
+//                     (else identity K columns); bf16 layer1 blocks as one
+//                     fused kernel (variant 40), as ResNet-18's plan
 //   Bottleneck:  T1 = relu(conv1x1(X));  T2 = relu(conv3x3/s(T1))
 //                downsample block: Y = relu(conv1x1(T2) + ds(X)) as one GEMM
 //                (K = width + cin, shortcut pixels (oy*s, ox*s) of X)
@@ -239,6 +242,16 @@ static int rn_block_conv(const sad_resnet_plan* p, const ConvW& c, const void* x
   return launch_block_conv(a, p->dtype, s);
 }
 
+// BasicBlock conv2 whose identity shortcut goes in as an epilogue residual
+// (ResNet-18's plan, api.hip run_blocks): stride 1, no downsample, 16 x 16
+// tiles, Cout <= 64, or Cout <= 128 where layer2 runs the halo / resident-weight
+// kernels (the split-bf16 mode's variant 31 takes the identity as K columns)
+static bool identity_epilogue(int dtype, const Block& b, int Ho) {
+  if (!(dtype == SAD_BF16 || dtype == SAD_BF16X3) || b.stride != 1 || b.has_ds || Ho % 16 != 0) return false;
+  return b.cout <= 64 || (b.cout <= 128 && layer2_halo() && !(dtype == SAD_BF16 && layer2_v31()) &&
+                          !(dtype == SAD_BF16X3 && x3_layer2_v31()));
+}
+
 static int rn_chunk(const sad_resnet_plan* p, const float* map, const float* img, int64_t n, float* feats, char* ws,
                     hipStream_t s, const float* img3 = nullptr) {
   const size_t ab = rn_act_bytes(p, n);
@@ -253,8 +266,32 @@ static int rn_chunk(const sad_resnet_plan* p, const float* map, const float* img
   for (const Block& b : p->blocks) {
     const int Ho = H / b.stride;
     if (p->block == SAD_BASIC_BLOCK) {
-      if ((rc = rn_block_conv(p, b.c1, X, n, H, b.stride, nullptr, 0, 0, 1, T1, s))) return rc;
-      if ((rc = rn_block_conv(p, b.c2, T1, n, Ho, 1, X, H, C, b.stride, Y, s))) return rc;
+      if (p->dtype == SAD_BF16 && b.stride == 1 && !b.has_ds && b.cin == 64 && b.cout == 64 && H % 16 == 0 &&
+          l1_fused()) {
+        // layer1: the whole BasicBlock as one kernel (variant 40), as ResNet-18's plan
+        L1BlockArgs f{};
+        f.x = (const u16*)X;
+        f.out = (u16*)Y;
+        f.N = (int)n;
+        f.H = f.W = H;
+        f.w1 = (const u16*)b.c1.w;
+        f.w1_ld = b.c1.ld;
+        f.b1 = b.c1.b;
+        f.w2 = (const u16*)b.c2.w;
+        f.w2_ld = b.c2.ld;  // 576 + the identity's 64 K columns (not read: the residual is the patch centre)
+        f.b2 = b.c2.b;
+        if ((rc = launch_l1block(f, s))) return rc;
+      } else {
+        if ((rc = rn_block_conv(p, b.c1, X, n, H, b.stride, nullptr, 0, 0, 1, T1, s))) return rc;
+        if (identity_epilogue(p->dtype, b, Ho)) {
+          // identity blocks of layer1/2: the shortcut as an epilogue add on the
+          // halo / resident-weight kernels (as ResNet-18's plan), not as identity
+          // K columns on the implicit GEMM
+          if ((rc = rn_block_conv(p, b.c2, T1, n, Ho, 1, nullptr, 0, 0, 1, Y, s, X))) return rc;
+        } else {
+          if ((rc = rn_block_conv(p, b.c2, T1, n, Ho, 1, X, H, C, b.stride, Y, s))) return rc;
+        }
+      }
     } else {
       if ((rc = rn_block_conv(p, b.c1, X, n, H, 1, nullptr, 0, 0, 1, T1, s))) return rc;
       if ((rc = rn_block_conv(p, b.c2, T1, n, H, b.stride, nullptr, 0, 0, 1, T2, s))) return rc;
