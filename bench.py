@@ -60,7 +60,7 @@ DOMINANT_KERNEL_PREFIX = 'sad::halo256r_kernel<'
 DOMINANT_DESC = ('sad::halo256r_kernel (variant 31): patch-resident 256-channel x 16x16-pixel conv, weights '
                  'streamed into registers; the stride-1 layer3/4 convs of a step (5 convs; layer3.0 conv2 + downsample '
                  'runs as two image-range launches at micro-batch 2,048, the last one fuses the average pool; the '
-                 'stride-2 convs stay on the 256x256 implicit GEMM, variant 13)')
+                 'stride-2 convs run on variants 43 (layer2) and 32 (layer3/4))')
 TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r04_pmc_traffic.json', 'r03_pmc_traffic.json')
                      if os.path.exists(os.path.join(ROOT, 'profiles', f))), '')
 FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats

@@ -775,17 +775,19 @@ static bool l2conv_ds_ok(const BlockConvArgs& a) {
          a.W % 16 == 0 && a.Ho == a.H && a.Wo == a.W && a.in1 && a.Cin1 == 64 && a.ss1 == 2 && a.H1 == 2 * a.H &&
          a.W1 == 2 * a.W && !a.res && !a.pool_out && !a.st_part;
 }
-// SAD_S2_PATCH=1 runs the stride-2 3x3 convs (the first conv of layer2/3/4's
-// first block) on the patch-resident variant 32 (halo256s2.hip) instead of the
-// implicit GEMM (variants 13 / 15).  Off by default: measured same-box at mb
-// 512, l2.c1 644 vs 523 us, l3.c1 344 vs 328, l4.c1 284 vs 276, and -1.6 % end
-// to end; its ablations put 29-35 % of its time in the patch DMA (75 gathered
-// 1-KB pieces per 32-channel chunk) and 17-25 % in the epilogue.  Tested
-// (test_gpu_blockconv.py).
+// SAD_S2_PATCH (default 1 since round 4; 0 = the implicit GEMM, variants 13 /
+// 15) runs the stride-2 3x3 convs that variant 43 does not take (layer3/4's
+// first conv, bf16) on the patch-resident variant 32 (halo256s2.hip).  Round 3
+// measured it slower at micro-batch 512 (l2.c1 644 vs 523 us, l3.c1 344 vs
+// 328, l4.c1 284 vs 276, -1.6 % end to end, with layer2's conv1 on it too; its
+// ablations put 29-35 % of its time in the patch DMA and 17-25 % in the
+// epilogue).  At the round-4 micro-batch of 2,048 with layer2's conv1 on
+// variant 43 it is +0.2 % end to end, 3 of 3 same-box rounds
+// (profiles/r04_s2patch_ab.log).  Tested (test_gpu_blockconv.py).
 static bool s2_patch() {
   static const bool v = [] {
     const char* e = getenv("SAD_S2_PATCH");
-    return e ? atoi(e) != 0 : false;
+    return e ? atoi(e) != 0 : true;
   }();
   return v;
 }
