@@ -405,6 +405,8 @@ def held_clock(clk, achieved, peak, peak_mhz=2400.0):
     dominant kernel's fraction of the MFMA peak at that clock."""
     if not clk:
         return None
+    if clk['samples'] < 3:  # a short run (profiling): the clock may not have settled
+        return {**clk, 'note': 'fewer than 3 samples: the timed region was too short for a held-clock figure'}
     at = peak * clk['sclk_mhz_median'] / peak_mhz
     return {**clk, 'peak_mhz': peak_mhz, 'peak_at_held_clock': round(at, 1),
             'frac_at_held_clock': round(achieved / at, 4),

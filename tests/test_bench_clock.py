@@ -47,3 +47,5 @@ def test_held_clock_fraction():
     assert abs(h['peak_at_held_clock'] - 2500.0 * 2080 / 2400) < 0.1
     assert abs(h['frac_at_held_clock'] - 1369.0 / (2500.0 * 2080 / 2400)) < 1e-4
     assert bench.held_clock(None, 1.0, 2.0) is None
+    short = bench.held_clock({'sclk_mhz_median': 2384, 'power_w_median': 351.0, 'samples': 1}, 1369.0, 2500.0)
+    assert 'frac_at_held_clock' not in short and 'note' in short
