@@ -233,9 +233,12 @@ int sad_resnet_run_img3(const sad_resnet_plan* plan, const float* img3, int64_t 
  * roofline of the dominant kernel): between begin and end, every block-conv
  * launch of sad_backbone_run* is bracketed by HIP events on its stream.  end()
  * synchronises those events and returns, for the launches of tile `variant`
- * (0 = all), the summed kernel time, the launch count and their algorithmic
- * FLOPs (2*M*Cout*K with K the conv taps [+ the downsample], never the
- * identity shortcut's columns). */
+ * (0 = all), the summed kernel time, the number of KERNEL launches (a conv
+ * whose operands pass the 2 GiB buffer range runs as several image-range
+ * launches inside one bracket; each counts, so total_ms / launches is the
+ * average kernel duration rocprofv3 reports) and their algorithmic FLOPs
+ * (2*M*Cout*K with K the conv taps [+ the downsample], never the identity
+ * shortcut's columns). */
 int sad_profile_begin(void);
 int sad_profile_end(int32_t variant, double* total_ms, int64_t* launches, double* flops);
 

@@ -310,6 +310,7 @@ struct ProfRec {
   int variant;
   double flops;
   hipEvent_t e0, e1;
+  int64_t kernels;  // kernel launches inside the bracket (image-range splits each count)
 };
 static std::mutex g_prof_mu;
 static bool g_prof_on = false;
@@ -317,11 +318,13 @@ static std::vector<ProfRec> g_prof;
 
 static int timed_block_conv(const BlockConvArgs& a, int dtype, hipStream_t s, double flops) {
   if (!g_prof_on) return launch_block_conv(a, dtype, s);
-  ProfRec r{default_block_variant(a, dtype), flops, nullptr, nullptr};
+  ProfRec r{default_block_variant(a, dtype), flops, nullptr, nullptr, 0};
   SAD_CHECK_HIP(hipEventCreate(&r.e0));
   SAD_CHECK_HIP(hipEventCreate(&r.e1));
   SAD_CHECK_HIP(hipEventRecord(r.e0, s));
+  const int64_t k0 = block_conv_kernel_launches();
   int rc = launch_block_conv(a, dtype, s);
+  r.kernels = block_conv_kernel_launches() - k0;
   SAD_CHECK_HIP(hipEventRecord(r.e1, s));
   std::lock_guard<std::mutex> lk(g_prof_mu);
   g_prof.push_back(r);
@@ -340,7 +343,7 @@ bool sad::l1_fused() {
 }
 static int timed_l1block(const L1BlockArgs& a, hipStream_t s, double flops) {
   if (!g_prof_on) return launch_l1block(a, s);
-  ProfRec r{40, flops, nullptr, nullptr};
+  ProfRec r{40, flops, nullptr, nullptr, 1};
   SAD_CHECK_HIP(hipEventCreate(&r.e0));
   SAD_CHECK_HIP(hipEventCreate(&r.e1));
   SAD_CHECK_HIP(hipEventRecord(r.e0, s));
@@ -390,7 +393,7 @@ extern "C" int sad_profile_end(int32_t variant, double* total_ms, int64_t* launc
       SAD_CHECK_HIP(hipEventElapsedTime(&t, r.e0, r.e1));
       ms += t;
       fl += r.flops;
-      ++n;
+      n += r.kernels;
     }
     (void)hipEventDestroy(r.e0);
     (void)hipEventDestroy(r.e1);

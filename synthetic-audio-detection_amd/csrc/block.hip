@@ -30,6 +30,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 #include <vector>
 
@@ -1021,6 +1022,9 @@ static int stamp_report(const BlockConvArgs& a, hipStream_t s) {
 }
 #endif
 
+static std::atomic<int64_t> g_block_conv_kernels{0};
+int64_t block_conv_kernel_launches() { return g_block_conv_kernels.load(std::memory_order_relaxed); }
+
 int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int variant) {
   SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16 || dtype == SAD_BF16X3, "dtype");
   const int ES = dtype == SAD_F32 ? 4 : 2;
@@ -1088,6 +1092,7 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   if (a.M == 0) return SAD_OK;
   const int v = variant > 0 ? variant : default_block_variant(a_in, dtype);
   SAD_REQUIRE(variant_fits(v, a.Cout), "variant's channel tile does not divide Cout");
+  g_block_conv_kernels.fetch_add(1, std::memory_order_relaxed);
   if (v == 30) {
     SAD_REQUIRE(dtype != SAD_F32 && halo256_ok(a_in), "variant 30: bf16 / split-bf16 3x3/s1/p1, Cout % 256, 16 x 16 tiles");
 #if SAD_STAMPS
