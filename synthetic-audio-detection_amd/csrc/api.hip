@@ -519,7 +519,10 @@ static int front_sub_batch(int dtype) {
     return e ? atoi(e) : -1;
   }();
   if (v >= 0) return v;
-  return dtype == SAD_BF16 && l1_fused() ? 256 : 32;
+  // split-bf16 (layer1 on variant 42): 64, +0.8 % over 32 in the parity mode
+  // (same box, 2 rounds; 128 and the whole micro-batch are slower,
+  // profiles/r04_x3_frontmb_ab.log)
+  return dtype == SAD_BF16 && l1_fused() ? 256 : dtype == SAD_BF16X3 ? 64 : 32;
 }
 
 static int run_chunk(const sad_backbone_plan* p, const float* map, const float* img, int64_t mb, float* feats,
