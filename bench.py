@@ -428,7 +428,7 @@ def main():
     ap.add_argument('--batch', type=int, default=2048, help='segments per GPU per step')
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'bf16x3', 'fp32'])
     ap.add_argument('--micro-batch', type=int, default=0,
-                    help='segments per backbone launch sequence (0: 2048 bf16, 256 bf16x3, 128 fp32); stem/layer1 '
+                    help='segments per backbone launch sequence (0: 2048 bf16, 512 bf16x3, 128 fp32); stem/layer1 '
                          'run in sub-batches of SAD_FRONT_MB (256 for bf16 with the fused layer1, else 32), layers 2-4 on the whole micro-batch')
     ap.add_argument('--parity-steps', type=int, default=0, help='timed steps of the bf16x3 parity mode '
                                                                 '(0: max(steps // 3, 3); -1: skip)')
@@ -459,7 +459,7 @@ def main():
     from sad import weights as sw
     gold = os.path.join(ROOT, 'tests', 'golden')
     sd = sw.merged_state_dict(0, HEADS, False, bn_stats=sw.load_bn_stats(os.path.join(gold, 'bn_stats_n6.npz')))
-    mbs = {'bf16': 2048, 'bf16x3': 256, 'fp32': 128}
+    mbs = {'bf16': 2048, 'bf16x3': 512, 'fp32': 128}
     B = args.batch
     pcm = torch.empty(B, SEG, dtype=torch.int16, device=dev)
     _lib.call('sad_synth_pcm', 0, rank * B, B, SEG, _lib.ptr(pcm), _lib.stream_handle(dev))
