@@ -52,8 +52,9 @@ BF16_PEAK_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3        # f32 MFMA = f32 vector peak (MI355X_MICROARCH.md)
 # The dominant kernel and its rocprof key in the committed PMC traffic file
 # bf16: variant 31 (csrc/halo256r.hip), the stride-1 layer3/4 convs of a
-# 2,048-segment step; the split-bf16 parity mode runs its split form on the same convs
-DOMINANT_VARIANT = {'bf16': 31, 'bf16x3': 31, 'fp32': 13}
+# 2,048-segment step; the split-bf16 parity mode runs variant 30's split form
+# (csrc/halo256.hip) on the same convs (round 4)
+DOMINANT_VARIANT = {'bf16': 31, 'bf16x3': 30, 'fp32': 13}
 # rocprof names the kernel with its template arguments ('sad::halo256r_kernel<256, false>|131072'); the
 # key is resolved by this name prefix (see dominant_traffic), so a template change cannot make it stale
 DOMINANT_KERNEL_PREFIX = 'sad::halo256r_kernel<'
@@ -567,7 +568,7 @@ def main():
                 'value': round(par['value'], 1), 'unit': 'segments/s', 'ms_per_step': round(par['ms'], 3),
                 'steps': p_steps, 'micro_batch': par_mode.mb,
                 'per_rank_ms_per_step': par['rank_ms_per_step'],
-                'roofline': {'kernel': 'halo256r_kernel (variant 31), split-bf16: the stride-1 layer3/4 convs', 'achieved': round(pexe, 1),
+                'roofline': {'kernel': 'halo256_kernel (variant 30), split-bf16: the stride-1 layer3/4 convs', 'achieved': round(pexe, 1),
                              'unit': 'TFLOP/s (bf16 MFMA executed = 3 x algorithmic)', 'peak': BF16_PEAK_TFLOPS,
                              'frac': round(pexe / BF16_PEAK_TFLOPS, 4), 'algorithmic_tflops': round(palg, 1),
                              'algorithmic_frac_of_f32_peak': round(palg / F32_PEAK_TFLOPS, 4), **pinfo,

@@ -858,8 +858,19 @@ static bool x3_rw() {
 // The stride-1 3x3 convs with Cout % 256 == 0 (layer3/4): bf16 runs the
 // patch-resident variant 31 (weights streamed into registers, one barrier per
 // 64-channel chunk; 6-10 % faster than variant 13 per launch, +3 % end to end
-// same-box), split-bf16 its split form too (round 4).  SAD_HALO256 (A/B
+// same-box); split-bf16 variant 30's split form (below).  SAD_HALO256 (A/B
 // switch): 0 = variant 13 for both, 1 = variant 30 for both, 2 = the default.
+// SAD_X3_HALO256: the split-bf16 parity mode's layer3/4 stride-1 convs on
+// variant 30 (default since round 4: its split form is +1.2 % end to end in the
+// parity mode over variant 31's, same box, 2 rounds, profiles/
+// r04_x3_halo256_ab.log) or 31; SAD_HALO256=0 still puts both modes on variant 13
+static int x3_halo256_variant() {
+  static const int v = [] {
+    const char* e = getenv("SAD_X3_HALO256");
+    return e ? atoi(e) : 30;
+  }();
+  return v;
+}
 static int halo256_mode() {
   static const int v = [] {
     const char* e = getenv("SAD_HALO256");
@@ -886,10 +897,10 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
     if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64 && x3_l1_variant() == 42) return 42;
     if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64 && x3_rw()) return 26;
     if (x3_layer2_v31() && a.Cout == 128 && halo31_ok(a)) return 31;
-    if (halo256_mode() == 1 && halo256_ok(a)) return 30;
-    // layer3/4 stride-1 convs: variant 31's split form (chosen whatever the
-    // grid size: its K order differs from variant 13's)
-    if (halo256_mode() == 2 && a.Cout % 256 == 0 && halo31_ok(a)) return 31;
+    // layer3/4 stride-1 convs: variant 30's split form (or 31's; chosen
+    // whatever the grid size: their K orders differ from variant 13's)
+    if (halo256_mode() != 0 && (halo256_mode() == 1 || x3_halo256_variant() == 30) && halo256_ok(a)) return 30;
+    if (halo256_mode() == 2 && x3_halo256_variant() == 31 && a.Cout % 256 == 0 && halo31_ok(a)) return 31;
     return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   }
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
