@@ -69,9 +69,13 @@ static_assert(SMEM_RES + 512 <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ int l2c_key(int x) { return (int)((l2c::KEY >> (3 * x)) & 7); }
 
-template <bool RES, bool DS, bool X3 = false>
+// ST (the trainer's raw conv, bf16 plain form): also the fused BN statistics,
+// fp32 sums of the accumulators and their squares per channel, one row of
+// a.st_part ([rows][2][128]) per workgroup
+template <bool RES, bool DS, bool X3 = false, bool ST = false>
 __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
   static_assert(!(RES && DS) && !(X3 && DS), "one shortcut form");
+  static_assert(!ST || (!RES && !DS && !X3), "statistics: the plain bf16 form");
   using namespace l2c;
   constexpr int TP = X3 ? 8 : 16;       // fragments (tile rows) per wave
   constexpr int UPT = 2 * TP;           // units per tap: (fragment, K-half)
@@ -89,7 +93,10 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
   const int tiles_x = a.W / 16, tiles_img = tiles_x * (a.H / 16);
   const int tiles_p = a.N * tiles_img;
   const int tp_begin = (int)((int64_t)w * tiles_p / gridDim.x), tp_end = (int)((int64_t)(w + 1) * tiles_p / gridDim.x);
-  if (tp_begin >= tp_end) return;  // whole workgroup (uniform)
+  if (tp_begin >= tp_end) {  // whole workgroup (uniform); its statistics row is zero
+    if constexpr (ST) a.st_part[(int64_t)w * 256 + tid] = 0.f;
+    return;
+  }
 
   const __amdgpu_buffer_rsrc_t rx =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
@@ -200,6 +207,9 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
     for (int j = 0; j < TP; ++j) acc[i][j] = b0;
   }
 
+  // ST: per-lane partial sums of channels cw + 16 i + 4 fg + e over this
+  // workgroup's pixels (column fr of every tile row), then across fr at the end
+  float st_s[2][4] = {}, st_q[2][4] = {};
   for (int t = tp_begin; t < tp_end; ++t) {
     const TileO o = tile_o(t);
     const TileO onext = tile_o(t + 1 < tp_end ? t + 1 : t);
@@ -414,6 +424,15 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
           v1[2] += __uint_as_float(r1.y << 16);
           v1[3] += __uint_as_float(r1.y & 0xFFFF0000u);
         }
+        if constexpr (ST) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            st_s[i][e] += v0[e];
+            st_s[i][e] += v1[e];
+            st_q[i][e] = fmaf(v0[e], v0[e], st_q[i][e]);
+            st_q[i][e] = fmaf(v1[e], v1[e], st_q[i][e]);
+          }
+        }
         uint32_t q[4] = {l1b_pk(v0[0], v0[1]), l1b_pk(v0[2], v0[3]), l1b_pk(v1[0], v1[1]), l1b_pk(v1[2], v1[3])};
         if (a.relu)
 #pragma unroll
@@ -435,6 +454,28 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
       }
     }
   }
+  if constexpr (ST) {
+    // across the 16 lanes (pixel columns) of each channel group, fixed order
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          st_s[i][e] += __shfl_xor(st_s[i][e], off, 64);
+          st_q[i][e] += __shfl_xor(st_q[i][e], off, 64);
+        }
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = cw + 16 * i + 4 * fg + e;
+          a.st_part[(int64_t)w * 256 + c] = st_s[i][e];
+          a.st_part[(int64_t)w * 256 + 128 + c] = st_q[i][e];
+        }
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -442,8 +483,10 @@ __global__ __launch_bounds__(256, 1) void l2conv_kernel(BlockConvArgs a) {
 // passes them: Cin 128 = 64 logical, Cout and the bias logical 64)
 int launch_l2conv(const BlockConvArgs& a, hipStream_t s, bool x3) {
   using namespace l2c;
-  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.pool_out && !a.st_part,
-              "variant 41/42: 3x3/s1/p1, no pool or statistics");
+  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.pool_out,
+              "variant 41/42: 3x3/s1/p1, no pool");
+  SAD_REQUIRE(!a.st_part || (!x3 && !a.in1 && !a.res && !a.relu && a.st_rows),
+              "variant 41 statistics: the plain bf16 raw conv (no shortcut / residual / ReLU), st_rows set");
   if (x3) {
     SAD_REQUIRE(!a.in1 && a.Cin == 128 && a.Cout == 64 && a.H % 16 == 0 && a.W % 16 == 0 && a.Ho == a.H &&
                     a.Wo == a.W && a.wt_ld >= 9 * 128 && a.wt_ld % 8 == 0 && a.in0_pstride % 64 == 0 &&
@@ -502,6 +545,15 @@ int launch_l2conv(const BlockConvArgs& a, hipStream_t s, bool x3) {
       attr = true;
     }
     hipLaunchKernelGGL((l2conv_kernel<false, true>), dim3((unsigned)g), dim3(256), SMEM_RES + 512, s, b);
+  } else if (a.st_part) {
+    static bool attr = false;
+    if (!attr) {
+      SAD_CHECK_HIP(hipFuncSetAttribute((const void*)l2conv_kernel<false, false, false, true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, OFF_RES + 512));
+      attr = true;
+    }
+    hipLaunchKernelGGL((l2conv_kernel<false, false, false, true>), dim3((unsigned)g), dim3(256), OFF_RES + 512, s, b);
+    *a.st_rows = (int)g;
   } else {
     static bool attr = false;
     if (!attr) {

@@ -856,6 +856,16 @@ extern "C" int sad_conv_bn_train_workspace_size(int64_t N, int32_t H, int32_t W,
   return SAD_OK;
 }
 
+// SAD_TRAIN_L2_RW (default 1): the trainer's layer2 128 -> 128 raw convs on the
+// resident-weight variant 41 with fused statistics (round 4); 0 = variant 20
+static bool train_l2_rw() {
+  static const bool v = [] {
+    const char* e = getenv("SAD_TRAIN_L2_RW");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* w_packed,
                                      int32_t Cout, int32_t k, int32_t stride, int32_t pad, int32_t dtype,
                                      const float* gamma, const float* beta, float eps, float momentum,
@@ -902,8 +912,11 @@ extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_
   // the patch-resident kernels (30, 31, 32, 43) sum no statistics; their
   // implicit-GEMM counterparts (13 / 15) do
   if ((v == 30 || v == 31 || v == 32 || v == 43) && dtype == SAD_BF16 && one_launch) v = gemm_block_variant(a);
-  if (v == 41 && dtype == SAD_BF16 && one_launch) v = 20;  // variant 41 sums no statistics either
-  const bool fused = dtype == SAD_BF16 && one_launch && (v == 13 || v == 15 || v == 20 || v == 25);
+  // variant 41 sums them in its plain form (no shortcut / residual: the
+  // trainer's raw convs of layer2's 128 -> 128 convs); SAD_TRAIN_L2_RW=0 keeps
+  // the weight-ring halo kernel (variant 20) there
+  if (v == 41 && dtype == SAD_BF16 && one_launch && (a.in1 || a.res || !train_l2_rw())) v = 20;
+  const bool fused = dtype == SAD_BF16 && one_launch && (v == 13 || v == 15 || v == 20 || v == 25 || v == 41);
   int rows = 0;
   if (fused) {
     a.st_part = ws;
