@@ -803,10 +803,11 @@ static bool l2s2_rw() {
   return v;
 }
 // variant 43's contract: 64 -> 128 3x3/s2/p1, output tiles 16 x 16, input
-// exactly twice the output, no shortcut / residual / pool / statistics
+// exactly twice the output, no shortcut / residual / pool
+// (the trainer's raw conv may add fused statistics: launch_l2s2conv checks them)
 static bool l2s2_ok(const BlockConvArgs& a) {
   return a.KH == 3 && a.KW == 3 && a.stride == 2 && a.pad == 1 && a.Cin == 64 && a.Cout == 128 && a.Ho % 16 == 0 &&
-         a.Wo % 16 == 0 && a.H == 2 * a.Ho && a.W == 2 * a.Wo && !a.in1 && !a.res && !a.pool_out && !a.st_part;
+         a.Wo % 16 == 0 && a.H == 2 * a.Ho && a.W == 2 * a.Wo && !a.in1 && !a.res && !a.pool_out;
 }
 bool layer2_halo() {
   static const bool v = [] {

@@ -69,6 +69,10 @@ static_assert(8 * ROWB + ODDC + 16 * PXB <= 65535, "fragment offsets are ds_read
 
 __device__ __forceinline__ int l2s_key(int x) { return (int)((l2s::KEY >> (3 * x)) & 7); }
 
+// ST (the trainer's raw conv): also the fused BN statistics, fp32 sums of the
+// accumulators and their squares per channel, one row of a.st_part
+// ([rows][2][128]) per workgroup
+template <bool ST = false>
 __global__ __launch_bounds__(256, 1) void l2s2conv_kernel(BlockConvArgs a) {
   using namespace l2s;
   const int ab = a.ablate;  // timing ablations (wrong results): 32 no patch DMA in the loop, 8 no epilogue stores
@@ -81,7 +85,10 @@ __global__ __launch_bounds__(256, 1) void l2s2conv_kernel(BlockConvArgs a) {
   const int tiles_x = a.Wo / 16, tiles_img = tiles_x * (a.Ho / 16);
   const int tiles_p = a.N * tiles_img;
   const int tp_begin = (int)((int64_t)w * tiles_p / gridDim.x), tp_end = (int)((int64_t)(w + 1) * tiles_p / gridDim.x);
-  if (tp_begin >= tp_end) return;  // whole workgroup (uniform)
+  if (tp_begin >= tp_end) {  // whole workgroup (uniform); its statistics row is zero
+    if constexpr (ST) a.st_part[(int64_t)w * 256 + tid] = 0.f;
+    return;
+  }
 
   const __amdgpu_buffer_rsrc_t rx =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)a.in0_bytes, 0x00020000);
@@ -178,6 +185,9 @@ __global__ __launch_bounds__(256, 1) void l2s2conv_kernel(BlockConvArgs a) {
     for (int kh = 0; kh < 2; ++kh) L[kx][kh] = (kx == 1 ? ODDC : 0) + xp * PXB + (((4 * kh + fg) ^ key) << 4);
   }
 
+  // ST: per-lane partial sums of channels cw + 16 i + 4 fg + e over this
+  // workgroup's pixels, then across the 16 pixel lanes at the end
+  float st_s[2][4] = {}, st_q[2][4] = {};
   for (int t = tp_begin; t < tp_end; ++t) {
     const TileO o = tile_o(t);
     const TileO onext = tile_o(t + 1 < tp_end ? t + 1 : t);
@@ -240,6 +250,15 @@ __global__ __launch_bounds__(256, 1) void l2s2conv_kernel(BlockConvArgs a) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const f32x4 v0 = acc[i][j], v1 = acc[i][j + 1];
+          if constexpr (ST) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              st_s[i][e] += v0[e];
+              st_s[i][e] += v1[e];
+              st_q[i][e] = fmaf(v0[e], v0[e], st_q[i][e]);
+              st_q[i][e] = fmaf(v1[e], v1[e], st_q[i][e]);
+            }
+          }
           uint32_t q[4] = {l1b_pk(v0[0], v0[1]), l1b_pk(v0[2], v0[3]), l1b_pk(v1[0], v1[1]), l1b_pk(v1[2], v1[3])};
           if (a.relu)
 #pragma unroll
@@ -262,14 +281,36 @@ __global__ __launch_bounds__(256, 1) void l2s2conv_kernel(BlockConvArgs a) {
       }
     });
   }
+  if constexpr (ST) {
+    // across the 16 lanes (pixel columns) of each channel group, fixed order
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          st_s[i][e] += __shfl_xor(st_s[i][e], off, 64);
+          st_q[i][e] += __shfl_xor(st_q[i][e], off, 64);
+        }
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = cw + 16 * i + 4 * fg + e;
+          a.st_part[(int64_t)w * 256 + c] = st_s[i][e];
+          a.st_part[(int64_t)w * 256 + 128 + c] = st_q[i][e];
+        }
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 int launch_l2s2conv(const BlockConvArgs& a, hipStream_t s) {
   using namespace l2s;
-  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 2 && a.pad == 1 && !a.in1 && !a.res && !a.pool_out &&
-                  !a.st_part,
-              "variant 43: 3x3/s2/p1, no shortcut, residual, pool or statistics");
+  SAD_REQUIRE(a.KH == 3 && a.KW == 3 && a.stride == 2 && a.pad == 1 && !a.in1 && !a.res && !a.pool_out,
+              "variant 43: 3x3/s2/p1, no shortcut, residual or pool");
+  SAD_REQUIRE(!a.st_part || (!a.relu && a.st_rows), "variant 43 statistics: the raw conv (no ReLU), st_rows set");
   SAD_REQUIRE(a.Cin == 64 && a.Cout == 128, "variant 43: Cin 64, Cout 128");
   SAD_REQUIRE(a.Ho % 16 == 0 && a.Wo % 16 == 0 && a.H == 2 * a.Ho && a.W == 2 * a.Wo,
               "variant 43: output must tile by 16 x 16, input twice its size");
@@ -282,12 +323,22 @@ int launch_l2s2conv(const BlockConvArgs& a, hipStream_t s) {
   BlockConvArgs b = a;
   b.out_bytes = ((int64_t)a.N * a.Ho * a.Wo - 1) * a.out_pstride * 2 + 256;
   SAD_REQUIRE(b.out_bytes < (1ll << 31) - 65536, "variant 43: output passes the 32-bit buffer range");
-  static bool attr = false;
-  if (!attr) {
-    SAD_CHECK_HIP(hipFuncSetAttribute((const void*)l2s2conv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
-    attr = true;
+  if (a.st_part) {
+    static bool attr = false;
+    if (!attr) {
+      SAD_CHECK_HIP(hipFuncSetAttribute((const void*)l2s2conv_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+      attr = true;
+    }
+    hipLaunchKernelGGL(l2s2conv_kernel<true>, dim3((unsigned)g), dim3(256), SMEM, s, b);
+    *a.st_rows = (int)g;
+  } else {
+    static bool attr = false;
+    if (!attr) {
+      SAD_CHECK_HIP(hipFuncSetAttribute((const void*)l2s2conv_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+      attr = true;
+    }
+    hipLaunchKernelGGL(l2s2conv_kernel<false>, dim3((unsigned)g), dim3(256), SMEM, s, b);
   }
-  hipLaunchKernelGGL(l2s2conv_kernel, dim3((unsigned)g), dim3(256), SMEM, s, b);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
 }

@@ -856,8 +856,9 @@ extern "C" int sad_conv_bn_train_workspace_size(int64_t N, int32_t H, int32_t W,
   return SAD_OK;
 }
 
-// SAD_TRAIN_L2_RW (default 1): the trainer's layer2 128 -> 128 raw convs on the
-// resident-weight variant 41 with fused statistics (round 4); 0 = variant 20
+// SAD_TRAIN_L2_RW (default 1): the trainer's layer2 raw convs on the
+// resident-weight variants with fused statistics (round 4): 128 -> 128 on
+// variant 41, the stride-2 64 -> 128 on variant 43; 0 = variants 20 / 15
 static bool train_l2_rw() {
   static const bool v = [] {
     const char* e = getenv("SAD_TRAIN_L2_RW");
@@ -909,14 +910,16 @@ extern "C" int sad_conv_bn_train_run(const void* x, int64_t N, int32_t H, int32_
   // plain conv launches, then bn_reduce over the stored output.
   const int64_t es = dtype == SAD_F32 ? 4 : 2, lim = (1ll << 31) - 65536;
   const bool one_launch = N * H * W * Cin * es < lim && a.M * Cout * es < lim;
-  // the patch-resident kernels (30, 31, 32, 43) sum no statistics; their
+  // the patch-resident kernels (30, 31, 32) sum no statistics; their
   // implicit-GEMM counterparts (13 / 15) do
-  if ((v == 30 || v == 31 || v == 32 || v == 43) && dtype == SAD_BF16 && one_launch) v = gemm_block_variant(a);
+  // (variant 43 sums them, layer2.0's stride-2 conv1; SAD_TRAIN_L2_RW=0 keeps the implicit GEMM there)
+  if ((v == 30 || v == 31 || v == 32 || (v == 43 && !train_l2_rw())) && dtype == SAD_BF16 && one_launch)
+    v = gemm_block_variant(a);
   // variant 41 sums them in its plain form (no shortcut / residual: the
   // trainer's raw convs of layer2's 128 -> 128 convs); SAD_TRAIN_L2_RW=0 keeps
   // the weight-ring halo kernel (variant 20) there
   if (v == 41 && dtype == SAD_BF16 && one_launch && (a.in1 || a.res || !train_l2_rw())) v = 20;
-  const bool fused = dtype == SAD_BF16 && one_launch && (v == 13 || v == 15 || v == 20 || v == 25 || v == 41);
+  const bool fused = dtype == SAD_BF16 && one_launch && (v == 13 || v == 15 || v == 20 || v == 25 || v == 41 || v == 43);
   int rows = 0;
   if (fused) {
     a.st_part = ws;

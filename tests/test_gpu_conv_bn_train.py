@@ -21,7 +21,8 @@ DEV = 'cuda:0'
     ('bf16', 4, 64, 64, 64, 3, 1, 1, 1),       # layer1: halo variant 25
     ('bf16', 4, 32, 128, 128, 3, 1, 1, 1),     # layer2 stride 1: resident-weight variant 41 (round 4; 16 tiles)
     ('bf16', 64, 64, 128, 128, 3, 1, 1, 1),    # ... at the trainer's 64 segments: 1,024 tiles on 256 workgroups
-    ('bf16', 64, 64, 64, 128, 3, 2, 1, 1),     # layer2.0 conv1 at 64 segments: variant 15
+    ('bf16', 64, 64, 64, 128, 3, 2, 1, 1),     # layer2.0 conv1 at 64 segments: variant 43 (round 4; one tile per workgroup)
+    ('bf16', 64, 128, 64, 128, 3, 2, 1, 1),    # ... 1,024 tiles on 256 workgroups
     ('bf16', 64, 64, 64, 128, 1, 2, 0, 1),     # layer2.0 downsample: variant 15
     ('bf16', 64, 32, 256, 256, 3, 1, 1, 1),    # layer3 at 64 segments: variant 13
     ('bf16', 64, 16, 512, 512, 3, 1, 1, 1),    # layer4 at 64 segments: 128 tiles of 256x256 -> variant 15
