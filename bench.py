@@ -29,11 +29,7 @@ import argparse
 import json
 import os
 import platform
-import re
-import statistics
-import subprocess
 import sys
-import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -50,74 +46,35 @@ SEG = 128000
 BACKBONE_FLOP = 18.13e9        # ResNet-18 @512^2 with conv1's 3 identical channels folded (reference: 18.95e9)
 BF16_PEAK_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3        # f32 MFMA = f32 vector peak (MI355X_MICROARCH.md)
-# The dominant kernel and its rocprof key in the committed PMC traffic file
-# bf16: variant 31 (csrc/halo256r.hip), the stride-1 layer3/4 convs of a
-# 2,048-segment step; the split-bf16 parity mode runs variant 30's split form
-# (csrc/halo256.hip) on the same convs (round 4)
-DOMINANT_VARIANT = {'bf16': 31, 'bf16x3': 30, 'fp32': 13}
-# rocprof names the kernel with its template arguments ('sad::halo256r_kernel<256, false>|131072'); the
-# key is resolved by this name prefix (see dominant_traffic), so a template change cannot make it stale
-DOMINANT_KERNEL_PREFIX = 'sad::halo256r_kernel<'
-DOMINANT_DESC = ('sad::halo256r_kernel (variant 31): patch-resident 256-channel x 16x16-pixel conv, weights '
-                 'streamed into registers; the stride-1 layer3/4 convs of a step (5 convs; layer3.0 conv2 + downsample '
-                 'runs as two image-range launches at micro-batch 2,048, the last one fuses the average pool; the '
-                 'stride-2 convs run on variants 43 (layer2) and 32 (layer3/4))')
-TRAFFIC_JSON = next((os.path.join(ROOT, 'profiles', f) for f in ('r04_pmc_traffic.json', 'r03_pmc_traffic.json')
-                     if os.path.exists(os.path.join(ROOT, 'profiles', f))), '')
+# The dominant kernel of each mode: (libsad profile variant, rocprof name prefix
+# (every template instantiation is launch-weighted, see dominant_traffic, so a
+# template change cannot make the key stale), what it is, the committed PMC
+# traffic file of that mode written by tools/profile_bench.sh)
+DOMINANT = {
+    'bf16': (31, 'sad::halo256r_kernel<',
+             'sad::halo256r_kernel (variant 31): patch-resident 256-channel x 16x16-pixel conv, weights streamed '
+             'into registers; the stride-1 layer3/4 convs of a step (5 convs; layer3.0 conv2 + downsample runs as '
+             'two image-range launches at micro-batch 2,048, the last one fuses the average pool)',
+             ('r05_pmc_traffic.json', 'r04_pmc_traffic.json')),
+    'bf16x3': (30, 'sad::halo256_kernel<',
+               'sad::halo256_kernel (variant 30), split-bf16: patch-resident 256-channel x 16x16-pixel conv; the '
+               'stride-1 layer3/4 convs (the last one fuses the average pool)',
+               ('r05_pmc_traffic_bf16x3.json',)),
+    'fp32': (13, 'sad::block_conv_kernel<float', 'sad::block_conv_kernel (variant 13), f32 MFMA', ()),
+}
+
+
+def traffic_file(dtype):
+    return next((os.path.join(ROOT, 'profiles', f) for f in DOMINANT[dtype][3]
+                 if os.path.exists(os.path.join(ROOT, 'profiles', f))), '')
+
+
 FE_FLOP = 16.4e6               # per segment: window, rFFT 2.5 N log2 N x 251, |X|^2, mel, dB, stats
 FE_BYTES = 256000 + 128512     # int16 PCM read + fp32 [128, 251] map written
 HEADS = 6
 
 
-class ClockSampler:
-    """Shader clock and package power from `rocm-smi` (a daemon thread) while
-    the timed steps run.  The board holds a power-limited clock in this loop
-    ('The power cap'), so the dense MFMA peak at that clock is
-    the ceiling the kernels face; `roofline.clock` reports it next to the
-    2.4 GHz `peak`.  Best effort: no rocm-smi, no samples -> None."""
-
-    def __init__(self, local_rank: int):
-        vis = os.environ.get('ROCR_VISIBLE_DEVICES') or os.environ.get('HIP_VISIBLE_DEVICES') or ''
-        ids = [v for v in vis.split(',') if v.strip().isdigit()]
-        self.gpu = int(ids[local_rank]) if local_rank < len(ids) else local_rank
-        self.samples, self._stop, self._th = [], threading.Event(), None
-
-    def _loop(self):
-        while not self._stop.is_set():
-            try:
-                txt = subprocess.run(['rocm-smi', '--showclocks', '--showpower'], capture_output=True, text=True,
-                                     timeout=10).stdout
-            except Exception:
-                return
-            sclk, power = {}, {}
-            for line in txt.splitlines():
-                m = re.match(r'GPU\[(\d+)\].*sclk clock level: \S+ \((\d+)Mhz\)', line)
-                if m:
-                    sclk[int(m.group(1))] = int(m.group(2))
-                m = re.match(r'GPU\[(\d+)\].*Graphics Package Power \(W\): ([\d.]+)', line)
-                if m:
-                    power[int(m.group(1))] = float(m.group(2))
-            g = self.gpu if self.gpu in sclk else (min(sclk) if sclk else None)
-            if g is not None:
-                self.samples.append((sclk[g], power.get(g)))
-            self._stop.wait(0.1)
-
-    def start(self):
-        self._th = threading.Thread(target=self._loop, daemon=True)
-        self._th.start()
-
-    def stop(self):
-        self._stop.set()
-        if self._th is not None:
-            self._th.join(timeout=12)
-        if not self.samples:
-            return None
-        pw = [p for _, p in self.samples if p is not None]
-        return {'sclk_mhz_median': statistics.median(s for s, _ in self.samples),
-                'power_w_median': statistics.median(pw) if pw else None, 'samples': len(self.samples)}
-
-
-def dominant_traffic(tr: dict, prefix: str = DOMINANT_KERNEL_PREFIX):
+def dominant_traffic(tr: dict, prefix: str = DOMINANT['bf16'][1]):
     """Memory-side bytes per launch (read + write) of the dominant kernel from a
     committed PMC traffic file (tools/profile_bench.sh): the launch-weighted mean
     over every record whose rocprof name starts with `prefix` (all template
@@ -277,6 +234,7 @@ class Mode:
             self.fe_done = [torch.cuda.Event(), torch.cuda.Event()]
             self.bb_done = [torch.cuda.Event(), torch.cuda.Event()]
             self.i = 0
+            self.primed = False
             self.fe_ev = [None, None]  # the events timing the front end that filled each slot
 
     def _frontend_ahead(self, pcm, slot, ev=None):
@@ -296,7 +254,7 @@ class Mode:
         # step's, whose front end starts now; the bench repeats one batch)
         if self.overlap:
             slot = self.i & 1
-            if self.i == 0:
+            if self.i == 0 and not self.primed:
                 self._frontend_ahead(pcm, slot)
             cur = torch.cuda.current_stream()
             cur.wait_event(self.fe_done[slot])
@@ -348,17 +306,21 @@ class Mode:
             bb.append(e[1].elapsed_time(e[2]))
         return sorted(fe)[reps // 2], sorted(bb)[reps // 2]
 
-    def run(self, pcm, steps, warmup, profile=True, clock=None):
+    def run(self, pcm, steps, warmup, profile=True):
         from sad import _lib
         for _ in range(warmup):
             self.step(pcm)
+        if self.overlap and self.i == 0:
+            # --warmup 0: the first timed step would run its own front end
+            # serially before its backbone (and the timed region would hold
+            # K + 1 front ends); prime slot 0 untimed instead
+            self._frontend_ahead(pcm, 0)
+            self.primed = True
         torch.cuda.synchronize()
         if self.world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
-        if clock is not None:
-            clock.start()
         t0 = time.perf_counter()
         for i in range(steps):
             if profile and i == steps - 1:
@@ -371,13 +333,12 @@ class Mode:
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        clk = clock.stop() if clock is not None else None
         k_ms, k_n, k_fl = _lib.ctypes.c_double(), _lib.I64(), _lib.ctypes.c_double()
-        _lib.call('sad_profile_end', DOMINANT_VARIANT[self.dtype] if profile else -1, _lib.ctypes.byref(k_ms),
+        _lib.call('sad_profile_end', DOMINANT[self.dtype][0] if profile else -1, _lib.ctypes.byref(k_ms),
                   _lib.ctypes.byref(k_n), _lib.ctypes.byref(k_fl))
         mean = lambda a, b: sum(e[a].elapsed_time(e[b]) for e in evs) / steps  # noqa: E731
         r = {'elapsed': elapsed, 'fe_ms': mean(0, 1), 'bb_ms': mean(5, 2), 'heads_ms': mean(2, 3),
-             'gather_ms': mean(3, 4), 'k_ms': k_ms.value, 'k_n': k_n.value, 'k_flop': k_fl.value, 'clock': clk}
+             'gather_ms': mean(3, 4), 'k_ms': k_ms.value, 'k_n': k_n.value, 'k_flop': k_fl.value}
         r['rank_ms_per_step'] = [round(elapsed * 1e3 / steps, 3)]
         r['rank_gather_ms'] = [round(r['gather_ms'], 4)]
         if self.world > 1:
@@ -401,17 +362,26 @@ def kernel_roofline(r, mfma_factor=1):
                                     'flop_per_launch': round(r['k_flop'] / n)}
 
 
-def held_clock(clk, achieved, peak, peak_mhz=2400.0):
-    """roofline.clock: the clock the board held during the timed steps and the
-    dominant kernel's fraction of the MFMA peak at that clock."""
-    if not clk:
-        return None
-    if clk['samples'] < 3:  # a short run (profiling): the clock may not have settled
-        return {**clk, 'note': 'fewer than 3 samples: the timed region was too short for a held-clock figure'}
-    at = peak * clk['sclk_mhz_median'] / peak_mhz
-    return {**clk, 'peak_mhz': peak_mhz, 'peak_at_held_clock': round(at, 1),
-            'frac_at_held_clock': round(achieved / at, 4),
-            'source': 'rocm-smi --showclocks --showpower sampled during the timed steps (rank 0)'}
+def gemm_reference(dev, n=16384, reps=5):
+    """hipBLASLt (torch.matmul) on a square bf16 GEMM, measured in this run on
+    this GPU: what the vendor's best plain GEMM reaches here, next to the
+    kernels' fractions of the 2.5 PFLOP/s spec (a reference point, not a peak)."""
+    a = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    b = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    for _ in range(2):
+        torch.matmul(a, b)
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.matmul(a, b)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    tf = 2.0 * n ** 3 / (min(ts) * 1e-3) / 1e12
+    del a, b
+    return {'what': f'torch.matmul (hipBLASLt) bf16 {n}^3, random data, best of {reps}, measured in this run',
+            'tflops': round(tf, 1), 'frac_of_peak': round(tf / BF16_PEAK_TFLOPS, 4)}
 
 
 def decisions(merged):
@@ -466,9 +436,8 @@ def main():
     _lib.call('sad_synth_pcm', 0, rank * B, B, SEG, _lib.ptr(pcm), _lib.stream_handle(dev))
 
     head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world, overlap=bool(args.overlap_frontend))
-    sample_clock = rank == 0 and os.environ.get('SAD_BENCH_CLOCK', '1') != '0'  # 0: no rocm-smi sampling (A/B)
-    r = head.run(pcm, args.steps, args.warmup, clock=ClockSampler(local) if sample_clock else None)
-    if head.overlap:
+    r = head.run(pcm, args.steps, args.warmup)
+    if head.overlap and not args.kernels_only:
         # the stage rooflines from the stages run alone (overlapped, the side
         # stream's front end and the backbone stretch each other)
         r['fe_ms_overlapped'], r['bb_ms_overlapped'] = r['fe_ms'], r['bb_ms']
@@ -484,6 +453,7 @@ def main():
             par_mode = Mode(sd, dev, 'bf16x3', mbs['bf16x3'], B, world, overlap=bool(args.overlap_frontend))
             par = par_mode.run(pcm, p_steps, 1)
             if par_mode.overlap:
+                par['bb_ms_overlapped'] = par['bb_ms']
                 par['fe_ms'], par['bb_ms'] = par_mode.isolated(pcm, reps=3)
 
     if rank == 0:
@@ -514,10 +484,16 @@ def main():
         peak = BF16_PEAK_TFLOPS if args.dtype != 'fp32' else F32_PEAK_TFLOPS
         fac = 3 if args.dtype == 'bf16x3' else 1
         alg, exe, kinfo = kernel_roofline(r, fac)
-        traffic = None
-        if TRAFFIC_JSON and args.dtype == 'bf16':
-            with open(TRAFFIC_JSON) as f:
-                traffic = dominant_traffic(json.load(f))
+        def traffic_of(dtype):
+            tf = traffic_file(dtype)
+            if not tf:
+                return None, None
+            with open(tf) as f:
+                return dominant_traffic(json.load(f), DOMINANT[dtype][1]), os.path.relpath(tf, ROOT)
+
+        traffic, traffic_src = traffic_of(args.dtype)
+        traffic_unit = ('memory-side bytes per launch = L2-miss traffic, Infinity-Cache hits included '
+                        f'(FETCH_SIZE x2 + WRITE_SIZE, {traffic_src})')
         bb_alg = BACKBONE_FLOP * B / (r['bb_ms'] * 1e-3) / 1e12
         out = {
             'metric': '4s@32kHz segments/sec end-to-end (mel+ResNet+ensemble), 1/2/4/8 MI355X',
@@ -532,20 +508,17 @@ def main():
                        'micro_batch': head.mb, 'frontend_overlap': head.overlap, 'parallelism': f'dp{world}',
                        'per_rank_ms_per_step': r['rank_ms_per_step'], 'per_rank_allgather_ms': r['rank_gather_ms']},
             'roofline': {'bound': 'mfma',
-                         'kernel': DOMINANT_DESC,
+                         'kernel': DOMINANT[args.dtype][2],
                          'achieved': round(exe, 1), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(exe / peak, 4),
-                         'traffic': traffic, 'traffic_unit': 'memory-side bytes per launch = L2-miss traffic, Infinity-Cache hits '
-                                                             'included (FETCH_SIZE x2 + WRITE_SIZE, '
-                                                             + os.path.relpath(TRAFFIC_JSON, ROOT) + ')',
+                         'traffic': traffic, 'traffic_unit': traffic_unit,
                          **kinfo,
                          'backbone': {'achieved': round(bb_alg * fac, 1), 'frac': round(bb_alg * fac / peak, 4),
                                       'ms_per_step': round(r['bb_ms'], 3), 'flop_per_segment': BACKBONE_FLOP,
                                       'what': 'fused resize+stem + 16 block-conv GEMMs + avgpool, HIP events '
                                               'around the backbone call' + (' (run alone after the timed steps; '
                                               f'overlapped with the next front end: {r["bb_ms_overlapped"]:.3f} ms)'
-                                              if head.overlap else '')},
-                         'measured_gemm_ceiling_tflops': 1344.0,
-                         'clock': held_clock(r['clock'], exe, peak),
+                                              if 'bb_ms_overlapped' in r else '')},
+                         'gemm_reference': None if args.kernels_only or args.dtype == 'fp32' else gemm_reference(dev),
                          # front end (configs[1]): fused STFT/mel/dB + standardise, fp32 VALU-bound
                          # (16.4 MFLOP and 384,512 B per segment)
                          'frontend': {'ms_per_step': round(r['fe_ms'], 3),
@@ -557,23 +530,31 @@ def main():
                                       **({'overlapped_ms_per_step': round(r['fe_ms_overlapped'], 3),
                                           'what': 'timed alone after the timed steps; in them it runs on a side '
                                                   'stream during the previous step\'s backbone'}
-                                         if head.overlap else {})}},
+                                         if 'fe_ms_overlapped' in r else {})}},
             'accuracy': accuracy(head),
         }
         if par is not None:
             palg, pexe, pinfo = kernel_roofline(par, 3)
+            ptraffic, ptraffic_src = traffic_of('bf16x3')
             out['parity_mode'] = {
                 'dtype': 'bf16x3', 'what': 'split-bf16: hi/lo bf16 operands, 3 bf16 MFMAs per product, fp32 '
                                            'accumulate (north-star parity mode)',
                 'value': round(par['value'], 1), 'unit': 'segments/s', 'ms_per_step': round(par['ms'], 3),
                 'steps': p_steps, 'micro_batch': par_mode.mb,
                 'per_rank_ms_per_step': par['rank_ms_per_step'],
-                'roofline': {'kernel': 'halo256_kernel (variant 30), split-bf16: the stride-1 layer3/4 convs', 'achieved': round(pexe, 1),
+                'roofline': {'kernel': DOMINANT['bf16x3'][2], 'achieved': round(pexe, 1),
                              'unit': 'TFLOP/s (bf16 MFMA executed = 3 x algorithmic)', 'peak': BF16_PEAK_TFLOPS,
                              'frac': round(pexe / BF16_PEAK_TFLOPS, 4), 'algorithmic_tflops': round(palg, 1),
-                             'algorithmic_frac_of_f32_peak': round(palg / F32_PEAK_TFLOPS, 4), **pinfo,
+                             # a ratio, not a fraction: the f32-exact products run 3.x times faster than
+                             # the f32 MFMA / VALU peak allows
+                             'algorithmic_over_f32_peak_ratio': round(palg / F32_PEAK_TFLOPS, 4), **pinfo,
+                             'traffic': ptraffic,
+                             'traffic_unit': ('memory-side bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, '
+                                              f'{ptraffic_src})' if ptraffic_src else None),
                              'backbone_algorithmic_tflops': round(BACKBONE_FLOP * B / (par['bb_ms'] * 1e-3) / 1e12,
-                                                                  1)},
+                                                                  1),
+                             'backbone_executed_frac': round(3 * BACKBONE_FLOP * B / (par['bb_ms'] * 1e-3) / 1e12
+                                                             / BF16_PEAK_TFLOPS, 4)},
                 'accuracy': accuracy(par_mode) if par_mode is not head else out['accuracy']}
         if world == 1 and args.fp32_steps > 0 and args.dtype != 'fp32':
             f = Mode(sd, dev, 'fp32', mbs['fp32'], B, 1).run(pcm, args.fp32_steps, 1, profile=False)

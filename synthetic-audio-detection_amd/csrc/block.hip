@@ -1034,8 +1034,10 @@ static int stamp_report(const BlockConvArgs& a, hipStream_t s) {
 }
 #endif
 
-static std::atomic<int64_t> g_block_conv_kernels{0};
-int64_t block_conv_kernel_launches() { return g_block_conv_kernels.load(std::memory_order_relaxed); }
+// per host thread: a launch from another thread inside a caller's
+// before/after bracket (sad_profile_*) must not land in that caller's count
+static thread_local int64_t g_block_conv_kernels = 0;
+int64_t block_conv_kernel_launches() { return g_block_conv_kernels; }
 
 int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int variant) {
   SAD_REQUIRE(dtype == SAD_F32 || dtype == SAD_BF16 || dtype == SAD_BF16X3, "dtype");
@@ -1104,7 +1106,7 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   if (a.M == 0) return SAD_OK;
   const int v = variant > 0 ? variant : default_block_variant(a_in, dtype);
   SAD_REQUIRE(variant_fits(v, a.Cout), "variant's channel tile does not divide Cout");
-  g_block_conv_kernels.fetch_add(1, std::memory_order_relaxed);
+  ++g_block_conv_kernels;
   if (v == 30) {
     SAD_REQUIRE(dtype != SAD_F32 && halo256_ok(a_in), "variant 30: bf16 / split-bf16 3x3/s1/p1, Cout % 256, 16 x 16 tiles");
 #if SAD_STAMPS

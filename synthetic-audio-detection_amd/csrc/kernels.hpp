@@ -95,7 +95,7 @@ struct L1BlockArgs {
   uint64_t* stamps;      // diagnostic builds only (-DSAD_STAMPS): s_memtime per tile phase
 };
 int launch_l1block(const L1BlockArgs& a, hipStream_t s);
-int64_t block_conv_kernel_launches();  // kernels dispatched by launch_block_conv so far (image-range launches each count)
+int64_t block_conv_kernel_launches();  // kernels dispatched by launch_block_conv on this host thread so far (image-range launches each count)
 bool l1_fused();  // SAD_L1_FUSED (default 1): bf16 layer1 BasicBlocks on the fused kernel (ResNet-18 and the generic plan)
 
 struct StemArgs {

@@ -268,6 +268,10 @@ class TrainNet:
             self._packed[key] = t
         return t
 
+    def invalidate_packed(self):
+        """Drop every cached weight pack (after the parameters were overwritten)."""
+        self._packed.clear()
+
     def invalidate(self, prefix: str, keep_modes=()):
         for key in [k for k in self._packed if k[0].startswith(prefix) and k[1] not in keep_modes]:
             del self._packed[key]
@@ -630,6 +634,11 @@ class MixedNet(TrainNet):
         self.pre = pre
         self.dtype = 'mixed'
 
+    def invalidate_packed(self):
+        # both caches: the bf16 layer4 packs and the fp32 prefix packs of ``pre``
+        super().invalidate_packed()
+        self.pre._packed.clear()
+
     def _l4(self, blk) -> bool:
         return blk[0].startswith('layer4')
 
@@ -822,4 +831,4 @@ class Trainer:
             net.nbt[k] = int(torch.as_tensor(sd[f'{k}.num_batches_tracked']).item())
         for k in head_keys():
             net.head_sd[k] = torch.as_tensor(sd[f'head.{k}']).clone()
-        net._packed.clear()
+        net.invalidate_packed()

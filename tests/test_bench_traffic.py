@@ -4,19 +4,27 @@ stale and the driver's line carried traffic = null)."""
 import json
 import os
 
+import pytest
+
 import bench
 
 
 def test_traffic_file_committed():
-    assert bench.TRAFFIC_JSON and os.path.exists(bench.TRAFFIC_JSON)
+    tf = bench.traffic_file('bf16')
+    assert tf and os.path.exists(tf)
 
 
-def test_dominant_kernel_resolves_in_committed_traffic():
-    with open(bench.TRAFFIC_JSON) as f:
+@pytest.mark.parametrize('dtype', ['bf16', 'bf16x3'])
+def test_dominant_kernel_resolves_in_committed_traffic(dtype):
+    tf = bench.traffic_file(dtype)
+    if dtype == 'bf16x3' and not tf:
+        pytest.skip('no committed split-bf16 PMC traffic file yet')
+    with open(tf) as f:
         tr = json.load(f)
-    keys = [k for k in tr if k.startswith(bench.DOMINANT_KERNEL_PREFIX)]
-    assert keys, f'no {bench.DOMINANT_KERNEL_PREFIX}* record in {bench.TRAFFIC_JSON}'
-    t = bench.dominant_traffic(tr)
+    prefix = bench.DOMINANT[dtype][1]
+    keys = [k for k in tr if k.startswith(prefix)]
+    assert keys, f'no {prefix}* record in {tf}'
+    t = bench.dominant_traffic(tr, prefix)
     assert t is not None and t > 0
     # per-launch memory-side bytes of a 1,024-segment layer3/4 conv: between
     # the output map alone and 4x the algorithmic operand bytes

@@ -3,7 +3,10 @@ front end runs on a side stream during the previous step's backbone, two map
 buffers).  Every step must still see its own batch's maps: driven with
 alternating batches (step i processes batch i and starts batch i+1's front
 end), the merged logits of every pipelined step equal the sequential step's
-for that batch, bit for bit -- a stale or half-written map buffer would show."""
+for that batch, bit for bit -- a stale or half-written map buffer would show.
+The pipelined steps run back to back with no host synchronisation between
+them (each step's logits are copied out on the compute stream), so a missing
+wait on fe_done / bb_done or a map-buffer reuse race is free to show up."""
 import os
 import sys
 
@@ -37,8 +40,12 @@ def test_overlapped_frontend_matches_sequential():
     assert not torch.equal(ref[0], ref[1])
     ovl = bench.Mode(sd, dev, 'bf16', 64, B, 1, overlap=True)
     order = [0, 1, 1, 0, 1, 0, 0]
+    got = []
+    torch.cuda.synchronize()
     for i, k in enumerate(order):
         nxt = pcms[order[i + 1]] if i + 1 < len(order) else pcms[k]
         ovl.step(pcms[k], next_pcm=nxt)
-        torch.cuda.synchronize()
-        assert torch.equal(ovl.merged, ref[k]), f'step {i}'
+        got.append(ovl.merged.clone())  # on the compute stream, after this step's heads
+    torch.cuda.synchronize()
+    for i, k in enumerate(order):
+        assert torch.equal(got[i], ref[k]), f'step {i}'

@@ -86,3 +86,24 @@ def test_backbone_micro_batch_2048_equals_1024():
     _, m1024 = Engine(sd, DEV, dtype='bf16', micro_batch=1024).forward_pcm(pcm)
     torch.cuda.synchronize()
     assert torch.equal(m2048, m1024)
+
+
+def test_backbone_x3_micro_batch_512_equals_256():
+    """The parity mode at the bench's micro-batch (512 segments in split bf16:
+    layer1's output is 512 x 128^2 x 128 x 2 B = 2^31 B, past the 32-bit buffer
+    range, so layer2.0's convs run as split-bf16 image-range launches) against
+    two 256-segment micro-batches, bit for bit."""
+    import os
+
+    from conftest import GOLDEN
+    from sad import _lib, weights as sw
+    from sad.engine import Engine
+    sd = sw.merged_state_dict(0, 6, False, bn_stats=sw.load_bn_stats(os.path.join(GOLDEN, 'bn_stats_n6.npz')))
+    B = 512
+    pcm = torch.empty(B, 128000, dtype=torch.int16, device=DEV)
+    _lib.call('sad_synth_pcm', 13, 0, B, 128000, _lib.ptr(pcm), _lib.stream_handle(torch.device(DEV)))
+    _, m512 = Engine(sd, DEV, dtype='bf16x3', micro_batch=512).forward_pcm(pcm)
+    _, m256 = Engine(sd, DEV, dtype='bf16x3', micro_batch=256).forward_pcm(pcm)
+    torch.cuda.synchronize()
+    assert torch.isfinite(m512).all()
+    assert torch.equal(m512, m256)

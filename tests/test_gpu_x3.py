@@ -171,9 +171,9 @@ def test_logits_x3_match_reference(golden_frontend, golden_models, tag):
 
 
 def test_logits_x3_vs_fp32_device_batch():
-    """512 synthetic segments (micro-batch 256, SAD_FRONT_MB sub-batches of 32
-    -> every chunk boundary crossed): bf16x3 vs the fp32 device path, and the
-    decisions they imply."""
+    """512 synthetic segments (micro-batch 256, stem + layer1 in SAD_FRONT_MB
+    sub-batches of 64 -> every chunk boundary crossed): bf16x3 vs the fp32
+    device path, and the decisions they imply."""
     from oracle.decision import interpret_multihead_logits
     from sad import _lib
     from sad.engine import Engine
