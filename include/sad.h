@@ -80,7 +80,17 @@ typedef struct sad_frontend_cfg {
 
 typedef struct sad_frontend_plan sad_frontend_plan;
 
+/* The mel filterbank built on the host in float64 from cfg (htk triangles,
+ * optional slaney area norm), rounded once to fp32. */
 int sad_frontend_plan_create(const sad_frontend_cfg* cfg, sad_frontend_plan** out);
+/* The same with the caller's filterbank: fbank = HOST fp32 [n_fft/2 + 1][n_mels]
+ * (finite, >= 0; copied).  torchaudio builds its bank in fp32 arithmetic
+ * (melscale_fbanks, called by MelSpectrogram at inference_runner.py:158-166);
+ * the host layer passes that exact bank, so the device projects on the
+ * reference's weights, not on a more accurate rounding of the same triangles
+ * (which moves a mel bin next to a strong tone at a triangle's edge by up to
+ * 6e-3 dB). */
+int sad_frontend_plan_create_fb(const sad_frontend_cfg* cfg, const float* fbank, sad_frontend_plan** out);
 int sad_frontend_plan_destroy(sad_frontend_plan* plan);
 /* Number of STFT frames per segment (1 + n_samples / hop = 251). */
 int sad_frontend_frames(const sad_frontend_plan* plan, int32_t* n_frames);

@@ -77,10 +77,11 @@ def melscale_fbanks(n_freqs: int, f_min: float, f_max: float, n_mels: int,
 
 
 def power_spectrogram(wf: torch.Tensor, n_fft: int = 2048, hop: int = 512) -> torch.Tensor:
-    """torchaudio Spectrogram(power=2): [..., T] -> [..., n_fft//2+1, frames]."""
+    """torchaudio Spectrogram(power=2): [..., T] -> [..., n_fft//2+1, frames]
+    (in wf's dtype: fp32 as the reference; float64 for the tests' exact values)."""
     shape = wf.shape
     w2 = wf.reshape(-1, shape[-1])
-    window = torch.hann_window(n_fft)
+    window = torch.hann_window(n_fft, dtype=wf.dtype)
     spec = torch.stft(w2, n_fft=n_fft, hop_length=hop, win_length=n_fft, window=window,
                       center=True, pad_mode='reflect', normalized=False, onesided=True,
                       return_complex=True)
@@ -94,7 +95,7 @@ def mel_spectrogram(wf: torch.Tensor, sr: int = 32000, cfg: SpectrogramConfig | 
     cfg = cfg or SpectrogramConfig()
     spec = power_spectrogram(wf, cfg.n_fft, cfg.hop_length)
     fb = melscale_fbanks(cfg.n_fft // 2 + 1, float(cfg.f_min), float(cfg.f_max), cfg.n_mels, sr, norm)
-    return torch.matmul(spec.transpose(-1, -2), fb).transpose(-1, -2)
+    return torch.matmul(spec.transpose(-1, -2), fb.to(spec.dtype)).transpose(-1, -2)
 
 
 def amplitude_to_db(x: torch.Tensor, top_db: float | None = 80.0) -> torch.Tensor:
@@ -146,15 +147,18 @@ def waveform_to_spectrogram(waveform: torch.Tensor, sr: int, spec_cfg: Spectrogr
     return spec3.unsqueeze(0)
 
 
-def batch_maps(pcm_i16, sr: int = 32000, cfg: SpectrogramConfig | None = None):
+def batch_maps(pcm_i16, sr: int = 32000, cfg: SpectrogramConfig | None = None, dtype=torch.float32):
     """[n, 128000] int16 (numpy or torch) -> (mel_db [n,128,251], std map [n,128,251]).
 
     Each segment goes through the reference's per-window path separately (the
-    top-db clamp and the moments are per segment)."""
+    top-db clamp and the moments are per segment).
+    dtype float64 gives the same arithmetic without the fp32 rounding (the
+    filterbank too): what the tests measure both the device and the fp32
+    restatement against."""
     t = torch.as_tensor(pcm_i16)
     dbs, maps = [], []
     for i in range(t.shape[0]):
-        wf = t[i].to(torch.float32) / 32768.0
+        wf = t[i].to(dtype) / 32768.0
         d, m = segment_map(wf, sr, cfg)
         dbs.append(d[0])
         maps.append(m[0])

@@ -479,18 +479,21 @@ using namespace sad;
 
 struct sad_frontend_plan : sad::FrontendPlan {};
 
-extern "C" int sad_frontend_plan_create(const sad_frontend_cfg* cfg, sad_frontend_plan** out) {
+// fb: [n_fft / 2 + 1][n_mels] fp32, the mel filterbank the plan projects on
+static int frontend_plan_build(const sad_frontend_cfg* cfg, const float* fb_in, sad_frontend_plan** out) {
   SAD_REQUIRE(cfg && out, "null cfg/out");
   SAD_REQUIRE(cfg->n_fft == FE_NFFT, "only n_fft = 2048 is supported");
   SAD_REQUIRE(cfg->hop_length > 0 && cfg->n_mels > 0 && cfg->n_mels <= 1024, "hop/n_mels");
   SAD_REQUIRE(cfg->n_samples > FE_NFFT / 2, "n_samples must exceed n_fft/2 (reflect pad)");
+  const int n_freqs = FE_NFFT / 2 + 1;
+  std::vector<float> fb = fb_in ? std::vector<float>(fb_in, fb_in + (size_t)n_freqs * cfg->n_mels)
+                                : mel_fbank(n_freqs, cfg->f_min, cfg->f_max, cfg->n_mels, cfg->sample_rate,
+                                            cfg->norm_slaney != 0);
+  for (float v : fb) SAD_REQUIRE(v >= 0.f && v < 1e30f, "filterbank weights must be finite and >= 0");
   auto* p = new sad_frontend_plan();
   p->cfg = *cfg;
   p->n_frames = 1 + cfg->n_samples / cfg->hop_length;
   (void)hipGetDevice(&p->device);
-  const int n_freqs = FE_NFFT / 2 + 1;
-  std::vector<float> fb = mel_fbank(n_freqs, cfg->f_min, cfg->f_max, cfg->n_mels, cfg->sample_rate,
-                                    cfg->norm_slaney != 0);
   std::vector<int> st(cfg->n_mels), ln(cfg->n_mels), off(cfg->n_mels);
   std::vector<float> w;
   int lo = n_freqs, hi = -1;
@@ -589,6 +592,15 @@ extern "C" int sad_frontend_plan_create(const sad_frontend_cfg* cfg, sad_fronten
 #undef UP
   *out = p;
   return SAD_OK;
+}
+
+extern "C" int sad_frontend_plan_create(const sad_frontend_cfg* cfg, sad_frontend_plan** out) {
+  return frontend_plan_build(cfg, nullptr, out);
+}
+
+extern "C" int sad_frontend_plan_create_fb(const sad_frontend_cfg* cfg, const float* fbank, sad_frontend_plan** out) {
+  SAD_REQUIRE(fbank, "null filterbank");
+  return frontend_plan_build(cfg, fbank, out);
 }
 
 extern "C" int sad_frontend_plan_destroy(sad_frontend_plan* p) {

@@ -51,6 +51,7 @@ SIGNATURES = {
     'sad_last_error': (ctypes.c_char_p, []),
     'sad_version': (ctypes.c_char_p, []),
     'sad_frontend_plan_create': (ctypes.c_int, [ctypes.POINTER(FrontendCfg), ctypes.POINTER(P)]),
+    'sad_frontend_plan_create_fb': (ctypes.c_int, [ctypes.POINTER(FrontendCfg), P, ctypes.POINTER(P)]),
     'sad_frontend_plan_destroy': (ctypes.c_int, [P]),
     'sad_frontend_frames': (ctypes.c_int, [P, ctypes.POINTER(I32)]),
     'sad_frontend_run': (ctypes.c_int, [P, P, I64, I64, P, P, P]),

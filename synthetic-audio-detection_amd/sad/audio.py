@@ -134,6 +134,28 @@ def save_pcm16(path: str, pcm: np.ndarray, sr: int = 32000):
         w.writeframes(np.ascontiguousarray(pcm.T).astype('<i2').tobytes())
 
 
+def melscale_fbanks(n_freqs: int, f_min: float, f_max: float, n_mels: int, sample_rate: int,
+                    slaney: bool) -> torch.Tensor:
+    """The mel filterbank [n_freqs, n_mels] exactly as torchaudio builds it for
+    MelSpectrogram (inference_runner.py:158-166, norm='slaney'; trainer
+    submodel_trainer.py:97-104, norm=None): htk mel points, triangles and the
+    slaney area norm evaluated in torch fp32 arithmetic, op for op, so the
+    weights are torchaudio's to the bit.  Plan-time data for
+    sad_frontend_plan_create_fb (the device projects on these weights)."""
+    hz = torch.linspace(0, sample_rate // 2, n_freqs)  # fp32, torch's linspace
+    mel_lo = 2595.0 * math.log10(1.0 + f_min / 700.0)  # python float64 scalars
+    mel_hi = 2595.0 * math.log10(1.0 + f_max / 700.0)
+    pts = 700.0 * (10.0 ** (torch.linspace(mel_lo, mel_hi, n_mels + 2) / 2595.0) - 1.0)
+    gaps = pts[1:] - pts[:-1]
+    rel = pts.unsqueeze(0) - hz.unsqueeze(1)                 # [n_freqs, n_mels + 2]
+    rising = (-1.0 * rel[:, :-2]) / gaps[:-1]
+    falling = rel[:, 2:] / gaps[1:]
+    fb = torch.max(torch.zeros(1), torch.min(rising, falling))
+    if slaney:
+        fb *= (2.0 / (pts[2:n_mels + 2] - pts[:n_mels])).unsqueeze(0)
+    return fb
+
+
 def _sinc_resample_kernel(orig: int, new: int, gcd: int, lowpass_filter_width: int = 6, rolloff: float = 0.99,
                           device=None):
     orig //= gcd

@@ -89,8 +89,14 @@ class FrontEnd:
         cfg = _lib.FrontendCfg(sample_rate, n_fft, hop, n_mels, f_min, f_max, 1 if norm == 'slaney' else 0,
                                -1.0 if top_db is None else float(top_db), n_samples)
         self._plan = _lib.P()
+        # torchaudio's own fp32 filterbank (sad.audio.melscale_fbanks), not the
+        # library's float64 rounding of the same triangles
+        from .audio import melscale_fbanks
+        fb = melscale_fbanks(n_fft // 2 + 1, float(f_min), float(f_max), n_mels, sample_rate,
+                             norm == 'slaney').contiguous()
         with torch.cuda.device(self.device):
-            _lib.call('sad_frontend_plan_create', _lib.ctypes.byref(cfg), _lib.ctypes.byref(self._plan))
+            _lib.call('sad_frontend_plan_create_fb', _lib.ctypes.byref(cfg), fb.data_ptr(),
+                      _lib.ctypes.byref(self._plan))
         nf = _lib.I32()
         _lib.call('sad_frontend_frames', self._plan, _lib.ctypes.byref(nf))
         self.n_frames, self.n_mels, self.n_samples = nf.value, n_mels, n_samples

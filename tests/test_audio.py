@@ -140,3 +140,31 @@ def test_window_starts_match_slice_waveform():
         window = int(cfg.window_size * 32000)
         starts = list(ingest.window_starts(n, window, int((1 - cfg.overlap) * window)))
         assert [s / 32000 for s in starts] == ts
+
+
+def test_product_fbank_equals_torchaudio_restatement():
+    """sad.audio.melscale_fbanks (the bank the device plan projects on, via
+    sad_frontend_plan_create_fb) is the oracle's torchaudio restatement bit for
+    bit, for the inference ('slaney') and trainer (None) banks -- and differs
+    from the library's float64-rounded default bank (the reason it exists)."""
+    import math
+
+    import torch
+
+    from oracle import frontend as ofe
+    from sad.audio import melscale_fbanks
+    for norm in ('slaney', None):
+        a = melscale_fbanks(1025, 20.0, 12000.0, 128, 32000, norm == 'slaney')
+        b = ofe.melscale_fbanks(1025, 20.0, 12000.0, 128, 32000, norm)
+        assert a.dtype == torch.float32 and torch.equal(a, b)
+    # the float64 evaluation of the same triangle, rounded once (what
+    # sad_frontend_plan_create builds): bin 130 of mel 59 differs by 1e-5 relative
+    hz2mel = lambda f: 2595.0 * math.log10(1.0 + f / 700.0)  # noqa: E731
+    lo, hi = hz2mel(20.0), hz2mel(12000.0)
+    pts = [700.0 * (10 ** ((lo + (hi - lo) * i / 129) / 2595.0) - 1.0) for i in range(130)]
+    k, m = 130, 59
+    f = 16000.0 * k / 1024
+    v = max(0.0, min((f - pts[m]) / (pts[m + 1] - pts[m]), (pts[m + 2] - f) / (pts[m + 2] - pts[m + 1])))
+    v *= 2.0 / (pts[m + 2] - pts[m])
+    a = melscale_fbanks(1025, 20.0, 12000.0, 128, 32000, True)
+    assert abs(float(a[k, m]) - v) > 1e-5 * v
