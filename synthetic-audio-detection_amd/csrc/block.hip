@@ -705,6 +705,8 @@ int launch_halo256s2(const BlockConvArgs& a, hipStream_t s);
 bool halo256s2_ok(const BlockConvArgs& a);
 int launch_halo_rw_x3(const BlockConvArgs& a, hipStream_t s);
 int launch_l2s2conv(const BlockConvArgs& a, hipStream_t s);
+int launch_halo256rs2(const BlockConvArgs& a, hipStream_t s, bool x3);
+bool halo256rs2_ok(const BlockConvArgs& a);
 
 // halo kernel (variant 20): bf16 stride-1 3x3 with Cout <= 128 (layer1, layer2's
 // second block), where the implicit GEMM is L2->LDS-fill bound (convbench,
@@ -785,10 +787,22 @@ static bool l2conv_ds_ok(const BlockConvArgs& a) {
 // epilogue).  At the round-4 micro-batch of 2,048 with layer2's conv1 on
 // variant 43 it is +0.2 % end to end, 3 of 3 same-box rounds
 // (profiles/r04_s2patch_ab.log).  Tested (test_gpu_blockconv.py).
-static bool s2_patch() {
-  static const bool v = [] {
+// Round 5: SAD_S2_PATCH=2 (the default) takes them to variant 44
+// (halo256rs2.hip: 64-channel chunks, whole 128-B lines per DMA piece, the
+// 33 x 33 patch single-buffered as four parity planes), 1 = variant 32.
+static int s2_patch() {
+  static const int v = [] {
     const char* e = getenv("SAD_S2_PATCH");
-    return e ? atoi(e) != 0 : true;
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+// SAD_X3_S2 (split-bf16): the stride-2 convs on variant 44's split form (44,
+// the default since round 5) or the split implicit GEMM (0: variants 13 / 15)
+static int x3_s2_variant() {
+  static const int v = [] {
+    const char* e = getenv("SAD_X3_S2");
+    return e ? atoi(e) : 44;
   }();
   return v;
 }
@@ -902,6 +916,9 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
     // whatever the grid size: their K orders differ from variant 13's)
     if (halo256_mode() != 0 && (halo256_mode() == 1 || x3_halo256_variant() == 30) && halo256_ok(a)) return 30;
     if (halo256_mode() == 2 && x3_halo256_variant() == 31 && a.Cout % 256 == 0 && halo31_ok(a)) return 31;
+    // the stride-2 convs (layer2/3/4's conv1): variant 44's split form (chosen
+    // whatever the grid size: its K order differs from the implicit GEMM's)
+    if (x3_s2_variant() == 44 && halo256rs2_ok(a)) return 44;
     return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   }
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights
@@ -927,7 +944,8 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
   if (dtype == SAD_BF16 && l2s2_rw() && l2s2_ok(a)) return 43;
   // the stride-2 3x3 convs: the patch-resident variant 32 (chosen whatever the
   // grid size, as above)
-  if (dtype == SAD_BF16 && s2_patch() && halo256s2_ok(a)) return 32;
+  if (dtype == SAD_BF16 && s2_patch() == 2 && halo256rs2_ok(a)) return 44;
+  if (dtype == SAD_BF16 && s2_patch() == 1 && halo256s2_ok(a)) return 32;
   return gemm_block_variant(a);
 }
 // the implicit-GEMM choice (also the fused-statistics path's: 30/31 sum no
@@ -956,7 +974,7 @@ bool block_conv_can_pool(const BlockConvArgs& a, int dtype) {
 static bool variant_fits(int v, int cout) {
   if (v == 26 || v == 42) return cout == 64;
   if (v == 30) return cout % 256 == 0;
-  if (v == 31 || v == 32) return cout % 128 == 0;
+  if (v == 31 || v == 32 || v == 44) return cout % 128 == 0;
   const int bc[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64, 128, 64, 128, 256, 128, 128, 64, 256, 128, 128};
   if (v == 20 || v == 21) return cout % 64 == 0;
   if (v == 22) return cout % 128 == 0;
@@ -1129,6 +1147,11 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   if (v == 32) {
     SAD_REQUIRE(dtype == SAD_BF16, "variant 32: bf16");
     return launch_halo256s2(a, s);
+  }
+  if (v == 44) {
+    SAD_REQUIRE((dtype == SAD_BF16 || dtype == SAD_BF16X3) && halo256rs2_ok(a_in),
+                "variant 44: bf16 / split-bf16 3x3/s2/p1, Cin % 64, Cout % 128, 16 x 16 output tiles");
+    return launch_halo256rs2(a, s, dtype == SAD_BF16X3);
   }
   if (v == 41) {
     SAD_REQUIRE(dtype == SAD_BF16 && (halo_ok(a_in, dtype) || l2conv_ds_ok(a_in)), "variant 41: bf16 3x3/s1/p1, H, W % 16");

@@ -113,6 +113,18 @@ CASES = [
     ('l2-s2-43-one-tile', 3, 32, 64, 128, 2, None, [43]),
     ('l2-s2-43', 2, 128, 64, 128, 2, None, [43]),
     ('l2-s2-43-many', 20, 128, 64, 128, 2, None, [43]),
+    # variant 44 (patch-resident stride-2 3x3 with 64-channel chunks in four
+    # parity planes, halo256rs2.hip; round 5): layer3/4's conv1 (the default)
+    # and layer2's (128-channel tiles: 4 channel groups x 2 pixel halves); one
+    # tile per image, few tiles (70 on 256 workgroups), many (1,200 on 256)
+    ('l3-s2-44', 3, 64, 128, 256, 2, None, [44]),
+    ('l4-s2-44', 5, 32, 256, 512, 2, None, [44]),
+    ('l3-s2-44-one-tile', 4, 32, 128, 256, 2, None, [44]),
+    ('l3-s2-44-ragged', 70, 32, 128, 256, 2, None, [44]),
+    ('l4-s2-44-many', 300, 32, 256, 512, 2, None, [44]),
+    ('l2-s2-44', 2, 128, 64, 128, 2, None, [44]),
+    ('l2-s2-44-many', 20, 64, 64, 128, 2, None, [44]),
+    ('l3-s2-44-rect-c384', 2, 64, 192, 384, 2, None, [44]),
 ]
 
 

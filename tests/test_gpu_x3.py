@@ -56,6 +56,11 @@ def _conv_ref(x, w, stride, pad, sc=None, wsc=None, sc_stride=1, bias=None, relu
     (128, 128, 16, 1, 'identity', 31),
     (64, 128, 32, 2, 'downsample', 31),
     (128, 128, 48, 1, None, 31),
+    # variant 44's split form (round 5): every stride-2 conv1 of the parity mode
+    (128, 256, 64, 2, None, 44),        # layer3.0 conv1
+    (256, 512, 32, 2, None, 44),        # layer4.0 conv1 (two channel tiles)
+    (64, 128, 128, 2, None, 44),        # layer2.0 conv1 (128-channel tiles)
+    (128, 256, 32, 2, None, 44),        # one tile per image
 ])
 def test_block_conv_x3_vs_float64(cin, cout, H, stride, shortcut, variant):
     from sad.engine import block_conv, from_split, to_split

@@ -233,3 +233,104 @@ def test_l2s2_reads_conflict_free_and_consistent():
                         # channels (4 kh + fg) * 8 .. + 7
                         assert wm[a] == (2 * j + ky, 2 * fr + kx, 4 * kh + fg), (ky, kx, kh, j, lane)
                     assert lds_cycles(addrs) == 4, (ky, kx, kh, j)
+
+
+# ---- variant 44 (csrc/halo256rs2.hip): a 16 x 16 output tile's 33 x 33 input
+# patch of a 64-channel chunk in four parity planes (EE, EO, OE, OO), each 17
+# pixel slots wide, 128 B per pixel, 16-B chunk c of plane column x at
+# c ^ key43(x); the chunk's 9 taps run plane by plane, and each plane's next
+# chunk is DMA'd by a per-tap schedule while the other planes' taps run
+NR44, NCV44, NP44 = [17, 17, 16, 16], [17, 16, 17, 16], [37, 37, 34, 34]
+OFF44, PITCH44 = [0, 37 * 1024, 74 * 1024, 108 * 1024], 17 * 128
+TPL44, TRO44, TCO44 = [0, 0, 0, 0, 1, 1, 2, 2, 3], [0, 0, 1, 1, 0, 1, 0, 0, 0], [0, 1, 0, 1, 0, 0, 0, 1, 0]
+TAP44 = [0, 2, 6, 8, 1, 7, 3, 5, 4]
+SCH44 = [[1 | 3 << 3, 2 | 1 << 3, -1], [1 | 4 << 3, 2 | 2 << 3, -1], [2 | 3 << 3, 3 | 0 << 3, -1],
+         [2 | 4 << 3, 3 | 1 << 3, -1], [0 | 4 | 0 << 3, 3 | 2 << 3, -1], [0 | 4 | 1 << 3, 3 | 3 << 3, -1],
+         [0 | 4 | 2 << 3, 1 | 4 | 0 << 3, 3 | 4 << 3], [0 | 4 | 3 << 3, 1 | 4 | 1 << 3, -1],
+         [0 | 4 | 4 << 3, 1 | 4 | 2 << 3, 2 | 4 | 0 << 3]]
+
+
+def v44_write_map():
+    """LDS byte -> (patch row, patch column, source chunk) or None, by the
+    kernel's issue() formulas."""
+    m = {}
+    for P in range(4):
+        for q in range(NP44[P]):
+            for ln in range(64):
+                u = 8 * q + (ln >> 3)
+                r = (u * 3856) >> 16
+                assert r == u // 17
+                x = u - 17 * r
+                ok = r < NR44[P] and x < NCV44[P]
+                a = OFF44[P] + q * 1024 + ln * 16
+                assert a not in m
+                m[a] = (2 * r + (P >> 1), 2 * x + (P & 1), (ln & 7) ^ key43(x)) if ok else None
+    assert max(m) + 16 <= 142 * 1024
+    return m
+
+
+def test_v44_patch_covers_window():
+    got = [v for v in v44_write_map().values() if v is not None]
+    assert len(got) == len(set(got))
+    assert set(got) == {(y, x, c) for y in range(33) for x in range(33) for c in range(8)}
+
+
+def test_v44_reads_conflict_free_and_consistent():
+    wm = v44_write_map()
+    for T in range(9):
+        ky, kx = divmod(TAP44[T], 3)
+        P = TPL44[T]
+        assert P == 2 * (ky & 1) + (kx & 1) and TRO44[T] == ky >> 1 and TCO44[T] == kx >> 1
+        for r0w in (0, 8):
+            for h in range(2):
+                for j in range(16 - r0w):
+                    addrs = []
+                    for lane in range(64):
+                        fr, fg = lane & 15, lane >> 4
+                        col = fr + TCO44[T]
+                        a = (OFF44[P] + TRO44[T] * PITCH44 + r0w * PITCH44 + col * 128
+                             + (((4 * h + fg) ^ key43(col)) << 4) + j * PITCH44)
+                        addrs.append(a)
+                        # output (r0w + j, fr) reads patch (2 (r0w + j) + ky, 2 fr + kx), chunk 4 h + fg
+                        assert wm[a] == (2 * (r0w + j) + ky, 2 * fr + kx, 4 * h + fg), (T, r0w, h, j, lane)
+                    assert lds_cycles(addrs) == 4, (T, r0w, h, j)
+
+
+def test_v44_dma_schedule():
+    """Every wave's pieces of every plane are issued once per chunk, after the
+    barrier that ends the plane's taps of the previous chunk and before the
+    barrier that opens its taps in this one (barriers at taps 0, 4, 6, 8)."""
+    first = {P: min(T for T in range(9) if TPL44[T] == P) for P in range(4)}
+    last = {P: max(T for T in range(9) if TPL44[T] == P) for P in range(4)}
+    bars = [0, 4, 6, 8]
+    nch = 3
+    for wave in range(8):
+        issued = {}  # (chunk, plane, k) -> global tap time of issue
+        for k in range(5):  # prologue: chunk 0's planes as the previous chunk's taps 4-8 would issue them
+            if k < 5:
+                issued[(0, 0, k)] = -1
+            if k < 3:
+                issued[(0, 1, k)] = -1
+        issued[(0, 2, 0)] = -1
+        for c in range(nch):
+            for T in range(9):
+                for d in SCH44[T]:
+                    if d < 0:
+                        continue
+                    P, nx, k = d & 3, (d >> 2) & 1, d >> 3
+                    if wave + 8 * k >= NP44[P]:
+                        continue
+                    key = (c + nx, P, k)
+                    assert key not in issued, key
+                    issued[key] = 9 * c + T
+        for c in range(nch):
+            for P in range(4):
+                need = [k for k in range(5) if wave + 8 * k < NP44[P]]
+                for k in need:
+                    tt = issued[(c, P, k)]
+                    open_bar = 9 * c + first[P]
+                    assert tt < open_bar, (wave, c, P, k)  # landed by the barrier that opens the plane
+                    if c > 0:
+                        # after the barrier following the previous chunk's last tap of the plane
+                        after = 9 * (c - 1) + min(b for b in bars + [9] if b > last[P])
+                        assert tt >= after, (wave, c, P, k, tt, after)
