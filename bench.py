@@ -258,6 +258,14 @@ class Mode:
                 self._frontend_ahead(pcm, slot)
             cur = torch.cuda.current_stream()
             cur.wait_event(self.fe_done[slot])
+            # ... and on everything the side stream holds now (this step's front
+            # end only: the next one is enqueued after the backbone).  On this
+            # runtime the event alone did not always order the backbone's first
+            # libsad launch behind a front end launched just before it (the
+            # backbone read a half-written map in 5-11 of 20 reps of
+            # tests/test_gpu_bench_overlap.py's sequence; with this wait 0 of 20,
+            # tools/overlap_repeat4.py)
+            cur.wait_stream(self.side)
             m = self.maps[slot]
         else:
             if ev is not None:

@@ -38,14 +38,18 @@ def test_overlapped_frontend_matches_sequential():
         torch.cuda.synchronize()
         ref.append(seq.merged.clone())
     assert not torch.equal(ref[0], ref[1])
-    ovl = bench.Mode(sd, dev, 'bf16', 64, B, 1, overlap=True)
     order = [0, 1, 1, 0, 1, 0, 0]
-    got = []
-    torch.cuda.synchronize()
-    for i, k in enumerate(order):
-        nxt = pcms[order[i + 1]] if i + 1 < len(order) else pcms[k]
-        ovl.step(pcms[k], next_pcm=nxt)
-        got.append(ovl.merged.clone())  # on the compute stream, after this step's heads
-    torch.cuda.synchronize()
-    for i, k in enumerate(order):
-        assert torch.equal(got[i], ref[k]), f'step {i}'
+    # 8 repetitions of the sequence: a cross-stream ordering hole shows in a
+    # fraction of them (before the fix in bench.Mode.step: 25-55 % of the
+    # repetitions had a step reading a half-written map)
+    for rep in range(8):
+        ovl = bench.Mode(sd, dev, 'bf16', 64, B, 1, overlap=True)
+        got = []
+        torch.cuda.synchronize()
+        for i, k in enumerate(order):
+            nxt = pcms[order[i + 1]] if i + 1 < len(order) else pcms[k]
+            ovl.step(pcms[k], next_pcm=nxt)
+            got.append(ovl.merged.clone())  # on the compute stream, after this step's heads
+        torch.cuda.synchronize()
+        for i, k in enumerate(order):
+            assert torch.equal(got[i], ref[k]), f'repetition {rep}, step {i}'
