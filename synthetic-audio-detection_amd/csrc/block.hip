@@ -787,22 +787,27 @@ static bool l2conv_ds_ok(const BlockConvArgs& a) {
 // epilogue).  At the round-4 micro-batch of 2,048 with layer2's conv1 on
 // variant 43 it is +0.2 % end to end, 3 of 3 same-box rounds
 // (profiles/r04_s2patch_ab.log).  Tested (test_gpu_blockconv.py).
-// Round 5: SAD_S2_PATCH=2 (the default) takes them to variant 44
-// (halo256rs2.hip: 64-channel chunks, whole 128-B lines per DMA piece, the
-// 33 x 33 patch single-buffered as four parity planes), 1 = variant 32.
+// Round 5: SAD_S2_PATCH=2 takes them to variant 44 (halo256rs2.hip: 64-channel
+// chunks, whole 128-B lines per DMA piece, the 33 x 33 patch single-buffered as
+// four parity planes).  It cuts variant 32's read amplification (rocprof, bench
+// pipeline: 1.20 vs 1.98 GB read per launch) but not its time (841 vs 773 us
+// per launch; convbench mb 1,024: l3.c1 675 vs 670 us, l4.c1 613 vs 564 us;
+// without any patch DMA still 3-6 % slower: four barriers per 64-channel
+// chunk against variant 32's one per 32), so variant 32 stays the default.
 static int s2_patch() {
   static const int v = [] {
     const char* e = getenv("SAD_S2_PATCH");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
-// SAD_X3_S2 (split-bf16): the stride-2 convs on variant 44's split form (44,
-// the default since round 5) or the split implicit GEMM (0: variants 13 / 15)
+// SAD_X3_S2=44 (split-bf16): the stride-2 convs on variant 44's split form
+// instead of the split implicit GEMM (variants 13 / 15, the default: convbench
+// mb 512, l2.c1 1,141 vs 1,081 us, l3.c1 725 vs 720, l4.c1 658 vs 602)
 static int x3_s2_variant() {
   static const int v = [] {
     const char* e = getenv("SAD_X3_S2");
-    return e ? atoi(e) : 44;
+    return e ? atoi(e) : 0;
   }();
   return v;
 }
