@@ -213,13 +213,17 @@ def ingest_leg(eng, dev, minutes: float = 2.0, reps: int = 3):
 
 
 class Mode:
-    """One engine configuration timed on this rank's resident PCM.
+    """One engine configuration timed on this rank's resident PCM: each step is
+    front end -> backbone -> heads (-> all-gather) on the current stream.
 
-    overlap: the next step's front end runs on a side stream while this step's
-    backbone runs (two map buffers; each step still computes its whole batch
-    through every stage, the front end just starts one step early)."""
+    (Round 4 ran the next step's front end on a side stream during this step's
+    backbone, +0.9 %.  Round 5's repeated hand-off test found the backbone
+    reading stale map lines in a fraction of the steps on this runtime, with
+    event waits, host waits or an explicit L2 invalidate on every XCD
+    (tools/overlap_repeat*.py), so every stage of a step now
+    runs on the one stream.)"""
 
-    def __init__(self, sd, dev, dtype, micro_batch, B, world, overlap=False):
+    def __init__(self, sd, dev, dtype, micro_batch, B, world):
         from sad.engine import Engine
         self.eng = Engine(sd, dev, dtype=dtype, micro_batch=micro_batch)
         self.dtype, self.mb, self.B, self.world, self.dev = dtype, micro_batch, B, world, dev
@@ -227,57 +231,14 @@ class Mode:
         self.logits = torch.empty(B, HEADS, 2, device=dev)
         self.merged = torch.empty(B, HEADS + 1, device=dev)
         self.gathered = torch.empty(world * B, HEADS + 1, device=dev) if world > 1 else None
-        self.overlap = overlap
-        if overlap:
-            self.side = torch.cuda.Stream(dev)
-            self.maps = [None, None]
-            self.fe_done = [torch.cuda.Event(), torch.cuda.Event()]
-            self.bb_done = [torch.cuda.Event(), torch.cuda.Event()]
-            self.i = 0
-            self.primed = False
-            self.fe_ev = [None, None]  # the events timing the front end that filled each slot
 
-    def _frontend_ahead(self, pcm, slot, ev=None):
-        # the slot's previous reader (the backbone two steps back) must be done
-        self.side.wait_event(self.bb_done[slot])
+    def step(self, pcm, ev=None):
         if ev is not None:
-            ev[0].record(self.side)
-        with torch.cuda.stream(self.side):
-            self.maps[slot] = self.eng.frontend(pcm, out=self.maps[slot])
+            ev[0].record()
+        m = self.eng.frontend(pcm)
         if ev is not None:
-            ev[1].record(self.side)
-        self.fe_done[slot].record(self.side)
-
-    def step(self, pcm, ev=None, next_pcm=None):
-        # (overlap: pcm is this step's batch -- its maps were computed during
-        # the previous step, except for the first -- and next_pcm the next
-        # step's, whose front end starts now; the bench repeats one batch)
-        if self.overlap:
-            slot = self.i & 1
-            if self.i == 0 and not self.primed:
-                self._frontend_ahead(pcm, slot)
-            cur = torch.cuda.current_stream()
-            cur.wait_event(self.fe_done[slot])
-            # ... and on everything the side stream holds now (this step's front
-            # end only: the next one is enqueued after the backbone).  On this
-            # runtime the event alone did not always order the backbone's first
-            # libsad launch behind a front end launched just before it (the
-            # backbone read a half-written map in 5-11 of 20 reps of
-            # tests/test_gpu_bench_overlap.py's sequence; with this wait 0 of 20,
-            # tools/overlap_repeat4.py)
-            cur.wait_stream(self.side)
-            m = self.maps[slot]
-        else:
-            if ev is not None:
-                ev[0].record()
-            m = self.eng.frontend(pcm)
-            if ev is not None:
-                ev[1].record()
-        if ev is not None:
-            ev[5].record()
+            ev[1].record()
         self.eng.backbones[0](m, out=self.feats)
-        if self.overlap:
-            self.bb_done[slot].record(cur)
         if ev is not None:
             ev[2].record()
         self.eng.heads([self.feats], self.logits, self.merged)
@@ -290,45 +251,16 @@ class Mode:
                 dist.all_gather(list(self.gathered.chunk(self.world)), self.merged)
         if ev is not None:
             ev[4].record()
-        if self.overlap:
-            # the next step's front end (its events time it on the side stream)
-            self._frontend_ahead(pcm if next_pcm is None else next_pcm, slot ^ 1, ev)
-            self.i += 1
-
-    def isolated(self, pcm, reps=5):
-        """Front end and backbone timed alone (sequentially, HIP events on the
-        current stream): the per-stage rooflines of an overlapped run, whose
-        concurrent stages stretch each other."""
-        cur = torch.cuda.current_stream()
-        torch.cuda.synchronize()
-        fe, bb = [], []
-        for _ in range(reps):
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            e[0].record(cur)
-            m = self.eng.frontend(pcm)
-            e[1].record(cur)
-            self.eng.backbones[0](m, out=self.feats)
-            e[2].record(cur)
-            torch.cuda.synchronize()
-            fe.append(e[0].elapsed_time(e[1]))
-            bb.append(e[1].elapsed_time(e[2]))
-        return sorted(fe)[reps // 2], sorted(bb)[reps // 2]
 
     def run(self, pcm, steps, warmup, profile=True):
         from sad import _lib
         for _ in range(warmup):
             self.step(pcm)
-        if self.overlap and self.i == 0:
-            # --warmup 0: the first timed step would run its own front end
-            # serially before its backbone (and the timed region would hold
-            # K + 1 front ends); prime slot 0 untimed instead
-            self._frontend_ahead(pcm, 0)
-            self.primed = True
         torch.cuda.synchronize()
         if self.world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(steps)]
         t0 = time.perf_counter()
         for i in range(steps):
             if profile and i == steps - 1:
@@ -345,7 +277,7 @@ class Mode:
         _lib.call('sad_profile_end', DOMINANT[self.dtype][0] if profile else -1, _lib.ctypes.byref(k_ms),
                   _lib.ctypes.byref(k_n), _lib.ctypes.byref(k_fl))
         mean = lambda a, b: sum(e[a].elapsed_time(e[b]) for e in evs) / steps  # noqa: E731
-        r = {'elapsed': elapsed, 'fe_ms': mean(0, 1), 'bb_ms': mean(5, 2), 'heads_ms': mean(2, 3),
+        r = {'elapsed': elapsed, 'fe_ms': mean(0, 1), 'bb_ms': mean(1, 2), 'heads_ms': mean(2, 3),
              'gather_ms': mean(3, 4), 'k_ms': k_ms.value, 'k_n': k_n.value, 'k_flop': k_fl.value}
         r['rank_ms_per_step'] = [round(elapsed * 1e3 / steps, 3)]
         r['rank_gather_ms'] = [round(r['gather_ms'], 4)]
@@ -412,9 +344,6 @@ def main():
     ap.add_argument('--parity-steps', type=int, default=0, help='timed steps of the bf16x3 parity mode '
                                                                 '(0: max(steps // 3, 3); -1: skip)')
     ap.add_argument('--fp32-steps', type=int, default=2, help='timed steps of the fp32 mode (N = 1; 0: skip)')
-    ap.add_argument('--overlap-frontend', type=int, default=1,
-                    help='1: each step\'s front end runs on a side stream during the previous step\'s backbone '
-                         '(the headline and parity modes)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--kernels-only', action='store_true',
                     help='profiling runs: only the headline mode (no parity/fp32 legs, accuracy or CPU baseline)')
@@ -443,13 +372,8 @@ def main():
     pcm = torch.empty(B, SEG, dtype=torch.int16, device=dev)
     _lib.call('sad_synth_pcm', 0, rank * B, B, SEG, _lib.ptr(pcm), _lib.stream_handle(dev))
 
-    head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world, overlap=bool(args.overlap_frontend))
+    head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world)
     r = head.run(pcm, args.steps, args.warmup)
-    if head.overlap and not args.kernels_only:
-        # the stage rooflines from the stages run alone (overlapped, the side
-        # stream's front end and the backbone stretch each other)
-        r['fe_ms_overlapped'], r['bb_ms_overlapped'] = r['fe_ms'], r['bb_ms']
-        r['fe_ms'], r['bb_ms'] = head.isolated(pcm)
     p_steps = max(args.steps // 3, 3) if args.parity_steps == 0 else args.parity_steps
     if args.kernels_only:
         p_steps, args.fp32_steps, args.no_cpu_baseline = -1, 0, True
@@ -458,11 +382,8 @@ def main():
         if args.dtype == 'bf16x3':
             par_mode, par = head, r
         else:
-            par_mode = Mode(sd, dev, 'bf16x3', mbs['bf16x3'], B, world, overlap=bool(args.overlap_frontend))
+            par_mode = Mode(sd, dev, 'bf16x3', mbs['bf16x3'], B, world)
             par = par_mode.run(pcm, p_steps, 1)
-            if par_mode.overlap:
-                par['bb_ms_overlapped'] = par['bb_ms']
-                par['fe_ms'], par['bb_ms'] = par_mode.isolated(pcm, reps=3)
 
     if rank == 0:
         from sad.engine import Engine
@@ -513,7 +434,7 @@ def main():
             'config': {'workload': 'end-to-end inference: B int16 4 s segments resident in HBM -> mel front end '
                                    '-> ResNet-18@512x512 -> 6 binary heads -> merge (+RCCL all-gather of logits)',
                        'segments_per_gpu_per_step': B, 'heads': HEADS, 'distinct_backbones': 1,
-                       'micro_batch': head.mb, 'frontend_overlap': head.overlap, 'parallelism': f'dp{world}',
+                       'micro_batch': head.mb, 'parallelism': f'dp{world}',
                        'per_rank_ms_per_step': r['rank_ms_per_step'], 'per_rank_allgather_ms': r['rank_gather_ms']},
             'roofline': {'bound': 'mfma',
                          'kernel': DOMINANT[args.dtype][2],
@@ -523,9 +444,7 @@ def main():
                          'backbone': {'achieved': round(bb_alg * fac, 1), 'frac': round(bb_alg * fac / peak, 4),
                                       'ms_per_step': round(r['bb_ms'], 3), 'flop_per_segment': BACKBONE_FLOP,
                                       'what': 'fused resize+stem + 16 block-conv GEMMs + avgpool, HIP events '
-                                              'around the backbone call' + (' (run alone after the timed steps; '
-                                              f'overlapped with the next front end: {r["bb_ms_overlapped"]:.3f} ms)'
-                                              if 'bb_ms_overlapped' in r else '')},
+                                              'around the backbone call in the timed steps'},
                          'gemm_reference': None if args.kernels_only or args.dtype == 'fp32' else gemm_reference(dev),
                          # front end (configs[1]): fused STFT/mel/dB + standardise, fp32 VALU-bound
                          # (16.4 MFLOP and 384,512 B per segment)
@@ -534,11 +453,7 @@ def main():
                                       'peak_tflops': F32_PEAK_TFLOPS,
                                       'frac': round(FE_FLOP * B / (r['fe_ms'] * 1e-3) / 1e12 / F32_PEAK_TFLOPS, 4),
                                       'achieved_gbps': round(FE_BYTES * B / (r['fe_ms'] * 1e-3) / 1e9, 1),
-                                      'segments_per_s': round(B / (r['fe_ms'] * 1e-3), 1),
-                                      **({'overlapped_ms_per_step': round(r['fe_ms_overlapped'], 3),
-                                          'what': 'timed alone after the timed steps; in them it runs on a side '
-                                                  'stream during the previous step\'s backbone'}
-                                         if 'fe_ms_overlapped' in r else {})}},
+                                      'segments_per_s': round(B / (r['fe_ms'] * 1e-3), 1)}},
             'accuracy': accuracy(head),
         }
         if par is not None:
