@@ -17,7 +17,9 @@
  *     sad_last_error() returns a thread-local message for the last failure;
  *   - all tensors are caller-owned device pointers (PyTorch caching allocator);
  *     the library never frees caller memory;
- *   - plans are opaque, immutable after creation, freed by *_destroy;
+ *   - plans are opaque, immutable after creation, freed by *_destroy (one
+ *     exception: the experimental fused front end's counters, see
+ *     sad_frontend_run);
  *   - *_run calls are asynchronous on the given hipStream_t (passed as void*),
  *     never allocate, never synchronise (graph-capturable);
  *   - distinct plans / streams may be used from different threads.
@@ -95,7 +97,13 @@ int sad_frontend_plan_destroy(sad_frontend_plan* plan);
 /* Number of STFT frames per segment (1 + n_samples / hop = 251). */
 int sad_frontend_frames(const sad_frontend_plan* plan, int32_t* n_frames);
 
-/* pcm: int16 mono segments, segment i at pcm + i*seg_stride (elements),
+/* Two kernels: fe_mel_db writes the dB map, fe_normalize standardises it.
+ * (SAD_FE_FUSED=1/2 selects an experimental one-kernel form in which the last
+ * workgroup of a segment standardises it, counting arrivals in the plan's
+ * per-segment counters; it measured 1.7-2.2x slower, DESIGN.md 5c.  With it,
+ * runs of ONE plan must not execute concurrently.)
+ *
+ * pcm: int16 mono segments, segment i at pcm + i*seg_stride (elements),
  *      n_samples each.  There is no n_ch argument: multi-channel audio goes
  *      through sad_pcm_mono_run first, once per file, as the reference
  *      averages the whole waveform before slicing it (inference_runner.py:145-146);

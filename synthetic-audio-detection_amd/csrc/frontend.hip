@@ -17,9 +17,17 @@
 //   consecutive int16 pairs (coalesced); reflect padding is index arithmetic.
 // Kernel 2 (fe_normalize): one workgroup per segment: max -> top-db clamp ->
 //   float64 mean / unbiased variance -> standardise (32,128 values).
+// Fused form (round 5, SAD_FE_FUSED=1/2, off by default: measured 1.7-2.2x
+//   slower): fe_mel_db's workgroups publish their block's dB tile
+//   and maximum, and the LAST workgroup of a segment to finish (a per-segment
+//   counter; 1: agent-scope release / acquire fences, 2: agent-scope stores and
+//   loads) standardises the whole segment -- fe_normalize's arithmetic in the
+//   same order, so the maps are bit-identical.  SAD_FE_XCD_MAP=1 orders the 1-D
+//   grid so a segment's 8 frame blocks share an XCD (neutral).
 #include <math.h>
 
 #include <algorithm>
+#include <functional>
 #include <vector>
 
 #include "common.hpp"
@@ -50,8 +58,15 @@ struct FrontendPlan {
   int* d_lane_tab = nullptr;
   float* d_lane_w = nullptr;
   int ml0 = 0, ml1 = 0;
+  // fused normalisation (staged plans): per-segment arrival counters (left at
+  // zero by every launch) and per-block maxima, for one launch chunk
+  unsigned* d_seg_cnt = nullptr;
+  float* d_seg_bmax = nullptr;
   int device = 0;
 };
+
+constexpr int FE_CHUNK = 65535;  // segments per launch (the non-fused grid's y limit)
+constexpr int kNormRegs = 32;    // normalisation: values per thread of 1,024 (maps up to 32,768 values)
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -103,10 +118,93 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 constexpr int FE_STAGE_MELS = 128;  // dB rows staged in LDS for coalesced stores
 constexpr int FE_POW = 800;         // power bins per wave in LDS (the reference's bank: 767)
+constexpr int FE_PWPAD = 8;         // zero slots before bin_lo (the mel windows' shifted starts)
 constexpr int FE_ZBUF = FE_NC + 16;  // spectrum slots per wave (fe_zslot padding)
 // LDS: twiddles 8 KB + 4 FFT buffers 32.5 KB + power 12.5 KB + dB staging 16.5 KB
 // = 70 KB: two workgroups per CU.  (The mel weights are read from the lane
 // table in global memory, L1-resident: 11.5 KB for the reference's bank.)
+
+// The fused form's tail: the segment's last workgroup standardises it.  The
+// values are visited as fe_normalize_kernel's 1,024 threads visit them
+// (virtual thread vt = tid + 256 j holds i = vt + 1024 k), and the float64
+// sums are reduced over the same butterflies and wave order, so both forms
+// give the same bits.
+template <bool SC1>  // SC1: agent-scope loads (global_load sc1: past the XCD's L2 to the coherence point)
+__device__ __forceinline__ float fe_ld(const float* p) {
+  if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+
+template <bool SC1>
+__device__ __forceinline__ void fe_standardise_segment(float* db, bool keep_db, float* y, int count,
+                                                       const float* bmax, int n_fb, float top_db, double* red) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float mx = -INFINITY;
+  for (int b = 0; b < n_fb; ++b) mx = fmaxf(mx, fe_ld<SC1>(bmax + b));
+  const float floor_db = top_db >= 0.f ? mx - top_db : -INFINITY;
+  // one virtual thread's 32 values at a time (the segment is re-read from L2
+  // per pass rather than held: 128 registers would spill)
+  auto load = [&](int j, float (&v)[kNormRegs]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < kNormRegs; ++k) {
+      const int i = tid + 256 * j + 1024 * k;
+      v[k] = i < count ? fmaxf(fe_ld<SC1>(db + i), floor_db) : 0.f;
+    }
+  };
+  auto reduce = [&](double (&p)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      for (int o = 32; o > 0; o >>= 1) p[j] += __shfl_xor(p[j], o, 64);
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[wave + 4 * j] = p[j];
+    __syncthreads();
+    double t = 0.0;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    return t;
+  };
+  double part[4];
+  float v[kNormRegs];
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    load(j, v);
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kNormRegs; ++k)
+      if (tid + 256 * j + 1024 * k < count) s += (double)v[k];
+    part[j] = s;
+  }
+  const double mean = reduce(part) / count;
+  const float mean_f = (float)mean;
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    load(j, v);
+    double ss = 0.0;
+#pragma unroll
+    for (int k = 0; k < kNormRegs; ++k)
+      if (tid + 256 * j + 1024 * k < count) {
+        const double d = (double)v[k] - mean;
+        ss += d * d;
+      }
+    part[j] = ss;
+  }
+  const double var = reduce(part) / (count - 1);
+  const float denom = (float)sqrt(var) + 1e-6f;
+  // the last pass reads a value before it (in place, y == db) overwrites it
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    load(j, v);
+#pragma unroll
+    for (int k = 0; k < kNormRegs; ++k) {
+      const int i = tid + 256 * j + 1024 * k;
+      if (i < count) {
+        if (keep_db) db[i] = v[k];  // caller asked for the clamped dB map
+        y[i] = (v[k] - mean_f) / denom;
+      }
+    }
+  }
+}
 
 template <typename IT>  // int16_t PCM (scaled by 1/32768, torchaudio.load normalize) or float
 __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
@@ -116,15 +214,26 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     const float2* __restrict__ tw1024, const float* __restrict__ window, const int* __restrict__ mel_start,
     const int* __restrict__ mel_len, const int* __restrict__ mel_off, const float* __restrict__ mel_w, int nnz,
     int n_mels, int bin_lo, int bin_hi, const int* __restrict__ lane_tab, const float* __restrict__ lane_w, int ml0,
-    int ml1, float* __restrict__ out) {
+    int ml1, float* __restrict__ out, int64_t n_seg, int xcd_map, int fuse, float top_db, float* __restrict__ map_out,
+    unsigned* __restrict__ seg_cnt, float* __restrict__ seg_bmax) {
   __shared__ float2 s_tw[FE_NC];
   __shared__ float2 s_buf[FE_WAVES][FE_ZBUF];
   __shared__ float2 s_tw3[64];  // W64^{q k2} at [k2][q]
   __shared__ float s_pow[FE_WAVES][FE_POW];
   __shared__ float s_db[FE_STAGE_MELS][FE_FRAMES_PER_WG + 1];
+  __shared__ double s_red[16];
+  __shared__ int s_last;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t seg = blockIdx.y;
+  // 1-D grid.  xcd_map: workgroup L -> segment 8 (L / 8 / n_fb) + L % 8, frame
+  // block (L / 8) % n_fb, so a segment's blocks share L mod 8 (one XCD);
+  // else segment L / n_fb, block L % n_fb
+  const int n_fb = (n_frames + FE_FRAMES_PER_WG - 1) / FE_FRAMES_PER_WG;
+  const int64_t L = blockIdx.x;
+  const int64_t L8 = L >> 3;
+  const int64_t seg = xcd_map ? (L8 / n_fb) * 8 + (L & 7) : L / n_fb;
+  const int fb = (int)(xcd_map ? L8 % n_fb : L % n_fb);
+  if (seg >= n_seg) return;  // the grid is padded to a multiple of 8 segments
   // segment `seg` starts at sample seg_offs[seg] (windows of a long waveform,
   // sad_frontend_run_windows) or at seg * seg_stride
   // (offsets are clamped to [0, max_off]: a bad table cannot read out of bounds)
@@ -150,7 +259,8 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
       mm[q] = lane_tab[q * 64 + lane];
       mk0[q] = lane_tab[128 + q * 64 + lane];
     }
-    for (int i = bin_hi - bin_lo + 1 + lane; i < FE_POW; i += 64) s_pow[wave][i] = 0.f;
+    for (int i = bin_hi - bin_lo + 1 + FE_PWPAD + lane; i < FE_POW; i += 64) s_pow[wave][i] = 0.f;
+    if (lane < FE_PWPAD) s_pow[wave][lane] = 0.f;
   }
   __syncthreads();
 
@@ -164,7 +274,7 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
   const int fg4 = lane >> 2, fq = lane & 3;
   const int fbr = (fq == 1 ? 2 : fq == 2 ? 1 : fq);  // bit-reversed q (output block of the lane)
 
-  const int f_begin = blockIdx.x * FE_FRAMES_PER_WG;
+  const int f_begin = fb * FE_FRAMES_PER_WG;
   const int f_end = min(n_frames, f_begin + FE_FRAMES_PER_WG);
   float2* buf = s_buf[wave];
   float* pw = s_pow[wave];
@@ -288,14 +398,15 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
       if (k & 1) w2 = cmul(w2, make_float2(0.99999529380957619f, -0.0030679567629659761f));
       const float2 WO = cmul(w2, O);
       const float re = E.x + WO.x, im = E.y + WO.y;
-      pw[k - bin_lo] = re * re + im * im;
+      pw[k - bin_lo + FE_PWPAD] = re * re + im * im;
     }
     wave_lds_sync();
     if (staged) {
       // every lane runs ml0 + ml1 steps (no divergence, independent loads):
-      // the row's bins in order, then zero weights -- the same sums as the
-      // CSR loop, bit for bit; the rows are spread over the lanes so their
-      // start bins rarely share an LDS bank (plan_create)
+      // zero weights, the row's bins in order, zero weights -- the same sums as
+      // the CSR loop, bit for bit; each 32-lane group's window starts are
+      // distinct mod 32, so every step's ds_read_b32 is bank-conflict-free
+      // (plan_create's matching)
       const float* pa = pw + mk0[0];
       const float* pb = pw + mk0[1];
       const float* wa = lane_w + lane;
@@ -311,7 +422,7 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
       for (int m = lane; m < n_mels; m += 64) {
         const int k0 = mel_start[m], len = mel_len[m], off = mel_off[m];
         float acc = 0.f;
-        for (int q = 0; q < len; ++q) acc = fmaf(pw[k0 + q - bin_lo], mel_w[off + q], acc);
+        for (int q = 0; q < len; ++q) acc = fmaf(pw[k0 + q - bin_lo + FE_PWPAD], mel_w[off + q], acc);
         out[(seg * n_mels + m) * n_frames + t] = 10.0f * log10f(fmaxf(acc, 1e-10f));
       }
     }
@@ -323,7 +434,52 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     const int nf = f_end - f_begin;
     for (int i = tid; i < n_mels * FE_FRAMES_PER_WG; i += 256) {
       const int m = i / FE_FRAMES_PER_WG, f = i - m * FE_FRAMES_PER_WG;
-      if (f < nf) out[(seg * n_mels + m) * n_frames + f_begin + f] = s_db[m][f];
+      if (f < nf) {
+        float* o = out + (seg * n_mels + m) * n_frames + f_begin + f;
+        if (fuse == 2)  // agent-scope store: at the coherence point when it completes
+          __hip_atomic_store(o, s_db[m][f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          *o = s_db[m][f];
+      }
+    }
+    // (fuse is a kernel argument, not a template parameter: the same binary
+    // runs both forms, so their dB maps are bit-identical)
+    if (fuse) {
+      // the block's maximum, then publish (release) and count the arrival
+      float bm = -INFINITY;
+      for (int i = tid; i < n_mels * FE_FRAMES_PER_WG; i += 256) {
+        const int m = i / FE_FRAMES_PER_WG, f = i - m * FE_FRAMES_PER_WG;
+        if (f < nf) bm = fmaxf(bm, s_db[m][f]);
+      }
+      for (int o = 32; o > 0; o >>= 1) bm = fmaxf(bm, __shfl_xor(bm, o, 64));
+      float* s_bm = s_pow[0];  // the frames are done with the power buffers
+      __syncthreads();
+      if (lane == 0) s_bm[wave] = bm;
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_store(seg_bmax + seg * n_fb + fb, fmaxf(fmaxf(s_bm[0], s_bm[1]), fmaxf(s_bm[2], s_bm[3])),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // fuse 1: agent-scope release (L2 write-back); fuse 2: the tile went out
+      // by agent-scope stores, so waiting for their completion is the release
+      if (fuse == 2)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      else
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __syncthreads();
+      if (tid == 0)
+        s_last = __hip_atomic_fetch_add(seg_cnt + seg, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (unsigned)(n_fb - 1);
+      __syncthreads();
+      if (!s_last) return;
+      if (fuse != 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (tid == 0) __hip_atomic_store(seg_cnt + seg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int count = n_mels * n_frames;
+      float* db = out + seg * count;
+      float* y = map_out + seg * count;
+      if (fuse == 2)
+        fe_standardise_segment<true>(db, db != y, y, count, seg_bmax + seg * n_fb, n_fb, top_db, s_red);
+      else
+        fe_standardise_segment<false>(db, db != y, y, count, seg_bmax + seg * n_fb, n_fb, top_db, s_red);
     }
   }
 }
@@ -339,7 +495,6 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
   return s;
 }
 
-constexpr int kNormRegs = 32;  // values per thread held in registers (1024 threads: maps up to 32768)
 __global__ __launch_bounds__(1024) void fe_normalize_kernel(float* db_io, int count,
                                                              float top_db, float* map_out) {
   __shared__ double red[16];
@@ -516,38 +671,86 @@ static int frontend_plan_build(const sad_frontend_cfg* cfg, const float* fb_in, 
   p->bin_hi = hi;
   p->nnz = (int)w.size();
   // lane table of the staged mel projection: the shorter half of the rows on
-  // q = 0, the longer on q = 1 (each padded to its longest row); within each,
-  // rows longest first into the 32-lane half (ds_read_b32 bank group) holding
-  // fewer rows whose start bin falls on the same bank
+  // q = 0, the longer on q = 1, each run over a window of its longest row's
+  // length ml[q].  A lane reads pw[start + i], i < ml[q], with one ds_read_b32
+  // per step; its 32-lane group (the instruction's bank group, bank = dword
+  // mod 32) is conflict-free when the group's window starts are distinct mod 32.
+  // Rows sorted by start bin alternate between the two groups, and each row's
+  // window may start d bins before the row (d <= ml[q] - len, zero weights in
+  // front; the power buffer has FE_PWPAD zero slots before bin_lo): a bipartite
+  // matching of rows to residues picks the d's.  For the reference's banks it
+  // matches every row (bank-conflict cycles of the projection 2.4x -> 1x, CPU
+  // model); an unmatched row keeps d = 0.  Leading zero products leave the fp32
+  // sums bit-identical.
   std::vector<int> lane_tab(256, 0);
   std::vector<float> lane_w;
-  bool lanes_ok = cfg->n_mels <= FE_STAGE_MELS && hi - lo < FE_POW;
+  bool lanes_ok = cfg->n_mels <= FE_STAGE_MELS && hi - lo + FE_PWPAD < FE_POW;
   if (lanes_ok) {
     std::vector<int> ord(cfg->n_mels);
     for (int m = 0; m < cfg->n_mels; ++m) ord[m] = m;
     std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return ln[x] < ln[y]; });
     const int nA = std::min(cfg->n_mels, 64);
     int ml[2] = {0, 0};
+    std::vector<int> lane_d(128, 0);
+    const char* me = getenv("SAD_FE_MATCH");  // 0: round 4's greedy split (A/B)
+    const bool match = !(me && atoi(me) == 0);
     for (int q = 0; q < 2; ++q) {
       std::vector<int> rows(q == 0 ? ord.begin() : ord.begin() + nA, q == 0 ? ord.begin() + nA : ord.end());
-      std::stable_sort(rows.begin(), rows.end(), [&](int x, int y) { return ln[x] > ln[y]; });
-      std::vector<int> grp[2];
-      for (int m : rows) {
-        int best = -1, bc = 1 << 30;
-        for (int g = 0; g < 2; ++g) {
-          if ((int)grp[g].size() >= 32) continue;
-          int c = 0;
-          for (int x : grp[g]) c += ((st[x] - lo) % 32 == (st[m] - lo) % 32) && st[x] != st[m];
-          if (c < bc) bc = c, best = g;
+      for (int m : rows) ml[q] = std::max(ml[q], ln[m]);
+      std::stable_sort(rows.begin(), rows.end(), [&](int x, int y) { return st[x] < st[y]; });
+      std::vector<int> grps[2];
+      if (match) {
+        for (size_t k = 0; k < rows.size(); ++k) grps[k & 1].push_back(rows[k]);
+      } else {  // round 4: longest first into the half with fewer same-bank starts
+        std::stable_sort(rows.begin(), rows.end(), [&](int x, int y) { return ln[x] > ln[y]; });
+        for (int m : rows) {
+          int best = -1, bc = 1 << 30;
+          for (int g = 0; g < 2; ++g) {
+            if ((int)grps[g].size() >= 32) continue;
+            int c = 0;
+            for (int x : grps[g]) c += ((st[x] - lo) % 32 == (st[m] - lo) % 32) && st[x] != st[m];
+            if (c < bc) bc = c, best = g;
+          }
+          grps[best].push_back(m);
         }
-        grp[best].push_back(m);
       }
-      for (int l = 0; l < 64; ++l) {
-        const int g = l >> 5, k = l & 31;
-        const int m = k < (int)grp[g].size() ? grp[g][k] : -1;
-        lane_tab[q * 64 + l] = m;
-        lane_tab[128 + q * 64 + l] = m >= 0 ? st[m] - lo : 0;
-        if (m >= 0) ml[q] = std::max(ml[q], ln[m]);
+      for (int g = 0; g < 2; ++g) {
+        const std::vector<int>& grp = grps[g];
+        // augmenting-path matching: row j -> residue (st - lo + PAD - d) mod 32
+        const int n = (int)grp.size();
+        std::vector<int> own(32, -1);
+        auto dmax = [&](int j) { return std::min(ml[q] - ln[grp[j]], st[grp[j]] - lo + FE_PWPAD); };
+        auto base = [&](int j) { return st[grp[j]] - lo + FE_PWPAD; };
+        std::vector<char> seen(32);
+        std::function<bool(int)> aug = [&](int j) {
+          for (int d = 0; d <= dmax(j); ++d) {
+            const int r = (base(j) - d) & 31;
+            if (seen[r]) continue;
+            seen[r] = 1;
+            if (own[r] < 0 || aug(own[r])) {
+              own[r] = j;
+              return true;
+            }
+          }
+          return false;
+        };
+        for (int j = 0; j < n && match; ++j) {
+          std::fill(seen.begin(), seen.end(), 0);
+          aug(j);
+        }
+        std::vector<int> dsel(n, 0);  // unmatched rows: d = 0
+        for (int r = 0; r < 32; ++r)
+          if (own[r] >= 0) dsel[own[r]] = (base(own[r]) - r) & 31;  // the least d with that residue
+        for (int j = 0; j < n; ++j) {
+          const int l = 32 * g + j;
+          lane_tab[q * 64 + l] = grp[j];
+          lane_tab[128 + q * 64 + l] = base(j) - dsel[j];
+          lane_d[q * 64 + l] = dsel[j];
+        }
+        for (int j = n; j < 32; ++j) {
+          lane_tab[q * 64 + 32 * g + j] = -1;
+          lane_tab[128 + q * 64 + 32 * g + j] = 0;
+        }
       }
     }
     for (int q = 0; q < 2 && lanes_ok; ++q)
@@ -558,7 +761,8 @@ static int frontend_plan_build(const sad_frontend_cfg* cfg, const float* fb_in, 
         for (int l = 0; l < 64; ++l) {
           const int m = lane_tab[q * 64 + l];
           if (m < 0) continue;
-          for (int i = 0; i < ln[m]; ++i) lane_w[(size_t)((q ? ml[0] : 0) + i) * 64 + l] = w[off[m] + i];
+          const int d = lane_d[q * 64 + l];
+          for (int i = 0; i < ln[m]; ++i) lane_w[(size_t)((q ? ml[0] : 0) + d + i) * 64 + l] = w[off[m] + i];
         }
       p->ml0 = ml[0];
       p->ml1 = ml[1];
@@ -588,6 +792,12 @@ static int frontend_plan_build(const sad_frontend_cfg* cfg, const float* fb_in, 
   if (lanes_ok) {
     UP(p->d_lane_tab, lane_tab);
     UP(p->d_lane_w, lane_w);
+    // the fused normalisation's counters (zero; each launch leaves them zero)
+    // and block maxima, for one launch chunk
+    const int n_fb = (p->n_frames + FE_FRAMES_PER_WG - 1) / FE_FRAMES_PER_WG;
+    std::vector<unsigned> zeros(FE_CHUNK, 0u);
+    UP(p->d_seg_cnt, zeros);
+    SAD_CHECK_HIP(hipMalloc((void**)&p->d_seg_bmax, (size_t)FE_CHUNK * n_fb * sizeof(float)));
   }
 #undef UP
   *out = p;
@@ -614,6 +824,8 @@ extern "C" int sad_frontend_plan_destroy(sad_frontend_plan* p) {
   (void)hipFree(p->d_mel_w);
   if (p->d_lane_tab) (void)hipFree(p->d_lane_tab);
   if (p->d_lane_w) (void)hipFree(p->d_lane_w);
+  if (p->d_seg_cnt) (void)hipFree(p->d_seg_cnt);
+  if (p->d_seg_bmax) (void)hipFree(p->d_seg_bmax);
   delete p;
   return SAD_OK;
 }
@@ -622,6 +834,26 @@ extern "C" int sad_frontend_frames(const sad_frontend_plan* p, int32_t* n) {
   SAD_REQUIRE(p && n, "null");
   *n = p->n_frames;
   return SAD_OK;
+}
+
+// SAD_FE_FUSED: 0 the two-kernel form (fe_mel_db + fe_normalize); 1 fused,
+// agent-scope release / acquire fences; 2 fused, the tiles stored and re-read
+// at agent scope (sc1) with no cache write-back / invalidate
+static int fe_fused() {
+  static const int v = [] {
+    const char* e = getenv("SAD_FE_FUSED");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+// SAD_FE_XCD_MAP=1: the XCD-aware block order (a segment's blocks on one XCD)
+static int fe_xcd_map() {
+  static const int v = [] {
+    const char* e = getenv("SAD_FE_XCD_MAP");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 template <typename IT>
@@ -637,19 +869,26 @@ static int frontend_run(const sad_frontend_plan* p, const IT* pcm, int64_t n_seg
   hipStream_t s = (hipStream_t)stream;
   float* dbbuf = out_db ? out_db : out_map;
   const int n_fb = (p->n_frames + FE_FRAMES_PER_WG - 1) / FE_FRAMES_PER_WG;
+  const int count = p->cfg.n_mels * p->n_frames;
+  const int fuse = p->d_seg_cnt != nullptr && count <= kNormRegs * 1024 ? fe_fused() : 0;
   int64_t done = 0;
-  while (done < n_seg) {  // gridDim.y <= 65535
-    const int64_t chunk = std::min<int64_t>(65535, n_seg - done);
-    const size_t off = (size_t)done * p->cfg.n_mels * p->n_frames;
-    hipLaunchKernelGGL(fe_mel_db_kernel<IT>, dim3(n_fb, (unsigned)chunk), dim3(256), 0, s,
+  while (done < n_seg) {
+    const int64_t chunk = std::min<int64_t>(FE_CHUNK, n_seg - done);
+    const size_t off = (size_t)done * count;
+    const int xmap = fe_xcd_map();
+    const unsigned blocks = (unsigned)((xmap ? (chunk + 7) / 8 * 8 : chunk) * n_fb);
+    hipLaunchKernelGGL(fe_mel_db_kernel<IT>, dim3(blocks), dim3(256), 0, s,
                        seg_offs ? pcm : pcm + done * seg_stride, seg_stride, seg_offs ? seg_offs + done : nullptr,
                        max_off, p->cfg.n_samples, p->n_frames, p->cfg.hop_length, p->d_tw1024, p->d_window,
                        p->d_mel_start, p->d_mel_len, p->d_mel_off, p->d_mel_w, p->nnz, p->cfg.n_mels, p->bin_lo,
-                       p->bin_hi, p->d_lane_tab, p->d_lane_w, p->ml0, p->ml1, dbbuf + off);
+                       p->bin_hi, p->d_lane_tab, p->d_lane_w, p->ml0, p->ml1, dbbuf + off, chunk, xmap, fuse, p->cfg.top_db,
+                       out_map + off, p->d_seg_cnt, p->d_seg_bmax);
     SAD_CHECK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(fe_normalize_kernel, dim3((unsigned)chunk), dim3(1024), 0, s, dbbuf + off,
-                       p->cfg.n_mels * p->n_frames, p->cfg.top_db, out_map + off);
-    SAD_CHECK_HIP(hipGetLastError());
+    if (!fuse) {
+      hipLaunchKernelGGL(fe_normalize_kernel, dim3((unsigned)chunk), dim3(1024), 0, s, dbbuf + off, count,
+                         p->cfg.top_db, out_map + off);
+      SAD_CHECK_HIP(hipGetLastError());
+    }
     done += chunk;
   }
   return SAD_OK;
