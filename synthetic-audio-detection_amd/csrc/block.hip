@@ -787,27 +787,30 @@ static bool l2conv_ds_ok(const BlockConvArgs& a) {
 // epilogue).  At the round-4 micro-batch of 2,048 with layer2's conv1 on
 // variant 43 it is +0.2 % end to end, 3 of 3 same-box rounds
 // (profiles/r04_s2patch_ab.log).  Tested (test_gpu_blockconv.py).
-// Round 5: SAD_S2_PATCH=2 takes them to variant 44 (halo256rs2.hip: 64-channel
-// chunks, whole 128-B lines per DMA piece, the 33 x 33 patch single-buffered as
-// four parity planes).  It cuts variant 32's read amplification (rocprof, bench
-// pipeline: 1.20 vs 1.98 GB read per launch) but not its time (841 vs 773 us
-// per launch; convbench mb 1,024: l3.c1 675 vs 670 us, l4.c1 613 vs 564 us;
-// without any patch DMA still 3-6 % slower: four barriers per 64-channel
-// chunk against variant 32's one per 32), so variant 32 stays the default.
+// Round 5: variant 44 (SAD_S2_PATCH=2, the default since round 5;
+// halo256rs2.hip: 64-channel chunks, whole 128-B lines per DMA piece, the
+// 33 x 33 patch single-buffered as four parity planes) reads the input once:
+// 1.20 vs 1.98 GB per bench launch (rocprof).  Its first form was slower (841 vs
+// 773 us per launch); with the tile decode hoisted out of the DMA issue and the
+// tap tables as SALU immediates: convbench mb 1,024 l3.c1 630 vs 682 us, l4.c1
+// 552 vs 553; end to end +0.2 % (2 of 3 same-box rounds,
+// profiles/r05_s2_ab.log).  SAD_S2_PATCH=1 keeps variant 32.
 static int s2_patch() {
   static const int v = [] {
     const char* e = getenv("SAD_S2_PATCH");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }
-// SAD_X3_S2=44 (split-bf16): the stride-2 convs on variant 44's split form
-// instead of the split implicit GEMM (variants 13 / 15, the default: convbench
-// mb 512, l2.c1 1,141 vs 1,081 us, l3.c1 725 vs 720, l4.c1 658 vs 602)
+// SAD_X3_S2 (split-bf16): 44 (default) runs layer3/4's stride-2 convs on
+// variant 44's split form, 0 on the split implicit GEMM (variants 13 / 15).
+// Convbench mb 512: l3.c1 692 vs 741 us, l4.c1 610 vs 617; layer2's conv1
+// (Cout 128) ties (1,071 vs 1,066) and stays on the GEMM; end to end neutral
+// (profiles/r05_s2_ab.log), kept for the bytes (1.2 vs 1.8-1.9 GB per launch).
 static int x3_s2_variant() {
   static const int v = [] {
     const char* e = getenv("SAD_X3_S2");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 44;
   }();
   return v;
 }
@@ -923,7 +926,7 @@ int default_block_variant(const BlockConvArgs& a, int dtype) {
     if (halo256_mode() == 2 && x3_halo256_variant() == 31 && a.Cout % 256 == 0 && halo31_ok(a)) return 31;
     // the stride-2 convs (layer2/3/4's conv1): variant 44's split form (chosen
     // whatever the grid size: its K order differs from the implicit GEMM's)
-    if (x3_s2_variant() == 44 && halo256rs2_ok(a)) return 44;
+    if (x3_s2_variant() == 44 && halo256rs2_ok(a) && a.Cout % 256 == 0) return 44;
     return halo_ok(a, dtype) && a.Cout <= 128 ? 20 : (a.Cout % 256 == 0 ? 13 : (a.Cout % 128 == 0 ? c128_variant() : 9));
   }
   if (halo_ok(a, dtype) && a.Cin == 64 && a.Cout == 64) return 25;  // layer1: resident weights

@@ -69,6 +69,26 @@ constexpr int SCH[9][3] = {
     {2 | 4 << 3, 3 | 1 << 3, -1}, {0 | 4 | 0 << 3, 3 | 2 << 3, -1}, {0 | 4 | 1 << 3, 3 | 3 << 3, -1},
     {0 | 4 | 2 << 3, 1 | 4 | 0 << 3, 3 | 4 << 3}, {0 | 4 | 3 << 3, 1 | 4 | 1 << 3, -1},
     {0 | 4 | 4 << 3, 1 | 4 | 2 << 3, 2 | 4 | 0 << 3}};
+// the tables above packed into 64-bit immediates, decoded by shifts of the
+// uniform tap index (SALU) instead of loads from a constant table
+constexpr uint64_t pack_sch(int e) {
+  uint64_t v = 0;
+  for (int T = 0; T < 9; ++T) v |= (uint64_t)(SCH[T][e] < 0 ? 0x7F : SCH[T][e]) << (7 * T);
+  return v;
+}
+constexpr uint64_t SCHP0 = pack_sch(0), SCHP1 = pack_sch(1), SCHP2 = pack_sch(2);
+constexpr uint64_t pack_step() {  // plane 2 bits | row offset 1 | column offset 1, per T
+  uint64_t v = 0;
+  for (int T = 0; T < 9; ++T) v |= (uint64_t)(TPL[T] | TRO[T] << 2 | TCO[T] << 3) << (4 * T);
+  return v;
+}
+constexpr uint64_t STEPP = pack_step();
+constexpr uint64_t pack_tap() {  // the next tap's index 3 ky + kx, per T < 8
+  uint64_t v = 0;
+  for (int T = 0; T < 8; ++T) v |= (uint64_t)TAP[T + 1] << (4 * T);
+  return v;
+}
+constexpr uint64_t TAPP = pack_tap();
 }  // namespace h44
 
 __device__ __forceinline__ int h44_key(int x) { return (int)((h44::KEY >> (3 * x)) & 7); }
@@ -138,22 +158,29 @@ __global__ __launch_bounds__(512, 1) void halo256rs2_kernel(BlockConvArgs a) {
   // pixels above / left of the image (the first patch row / column of a tile on
   // the image's top / left edge) load zeros; the right and bottom edges are
   // never crossed (the input is exactly twice the output).
-  auto issue = [&](int P, int t, int c, int k) __attribute__((always_inline)) {
-    const int q = wave + NW * k;
-    const int np = P < 2 ? 37 : 34, nr = P < 2 ? 17 : 16, ncv = (P & 1) ? 16 : 17;
-    if (q >= np || t >= tp_end) return;  // uniform
+  // a tile's image and input origin (decoded once per chunk, not per piece)
+  struct TileO {
+    int b, iy0, ix0;  // image, input row / column of the patch's slot (0, 0) minus the parity
+    bool ok;
+  };
+  auto tile_o = [&](int t) __attribute__((always_inline)) {
     const int tt = __builtin_amdgcn_readfirstlane(t);
     const int b = tt / tiles_img, rem = tt - b * tiles_img;
     const int ty = rem / tiles_x;
-    const int oy0 = ty * 16, ox0 = (rem - ty * tiles_x) * 16;
+    return TileO{b, 32 * ty - 1, 32 * (rem - ty * tiles_x) - 1, tt < tp_end};
+  };
+  auto issue = [&](int P, const TileO& to, int c, int k) __attribute__((always_inline)) {
+    const int q = wave + NW * k;
+    const int np = P < 2 ? 37 : 34, nr = P < 2 ? 17 : 16, ncv = (P & 1) ? 16 : 17;
+    if (q >= np || !to.ok) return;  // uniform
     int ln;  // opaque lane id: the per-piece slot math is not hoisted into registers
     asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
     const int u = 8 * q + (ln >> 3);
     const int r = (u * 3856) >> 16;  // u / 17, exact for u < 2000
     const int x = u - PW * r;
-    const int iy = 2 * oy0 - 1 + 2 * r + (P >> 1), ix = 2 * ox0 - 1 + 2 * x + (P & 1);
+    const int iy = to.iy0 + 2 * r + (P >> 1), ix = to.ix0 + 2 * x + (P & 1);
     const bool ok = r < nr && x < ncv && iy >= 0 && ix >= 0;
-    const int off = ((b * a.H + iy) * a.W + ix) * ps + c * 128 + (((ln & 7) ^ h44_key(x)) << 4);
+    const int off = ((to.b * a.H + iy) * a.W + ix) * ps + c * 128 + (((ln & 7) ^ h44_key(x)) << 4);
     const int poff = P == 0 ? OFF[0] : P == 1 ? OFF[1] : P == 2 ? OFF[2] : OFF[3];
     dma16_m0(r0, ok ? off : BAD, lds0 + poff + q * 1024);
   };
@@ -161,9 +188,12 @@ __global__ __launch_bounds__(512, 1) void halo256rs2_kernel(BlockConvArgs a) {
   // ---- prologue: the first chunk's planes as the previous chunk's taps 4-8
   // would have issued them (EE whole, EO pieces 0-2, OE piece 0); the loop
   // issues the rest while it runs
-  for (int k = 0; k < 5; ++k) issue(0, tp_begin, 0, k);
-  for (int k = 0; k < 3; ++k) issue(1, tp_begin, 0, k);
-  issue(2, tp_begin, 0, 0);
+  {
+    const TileO t0 = tile_o(tp_begin);
+    for (int k = 0; k < 5; ++k) issue(0, t0, 0, k);
+    for (int k = 0; k < 3; ++k) issue(1, t0, 0, k);
+    issue(2, t0, 0, 0);
+  }
   f32x4 biasv[TC];
 #pragma unroll
   for (int i = 0; i < TC; ++i) biasv[i] = *(const f32x4*)(a.bias + cw + i * 16 + fg * 4);
@@ -291,8 +321,10 @@ __global__ __launch_bounds__(512, 1) void halo256rs2_kernel(BlockConvArgs a) {
   //   T6 EE nxt 2, EO nxt 0, OO cur 4   T7 EE nxt 3, EO nxt 1   T8 EE nxt 4, EO nxt 2, OE nxt 0
   bool post_epi = false;
   for (int t = tp_begin; t < tp_end; ++t) {
+    const TileO tcur = tile_o(t), tnext = tile_o(t + 1);
     for (int c = 0; c < nch; ++c) {
-      const int nt = c + 1 < nch ? t : t + 1, ncn = c + 1 < nch ? c + 1 : 0;  // the next chunk
+      const int ncn = c + 1 < nch ? c + 1 : 0;  // the next chunk
+      const TileO& tn = c + 1 < nch ? tcur : tnext;
 #pragma unroll 1
       for (int T = 0; T < 9; ++T) {
         if (T == 0 || T == 4 || T == 6 || T == 8) {  // uniform
@@ -306,19 +338,23 @@ __global__ __launch_bounds__(512, 1) void halo256rs2_kernel(BlockConvArgs a) {
         }
         take_w();
         // the next step's weights (after the last tap: the next chunk's tap (0, 0))
-        const int kbn = T < 8 ? TAP[T + 1] * cinb + c * 128 : ncn * 128;
+        const int kbn = T < 8 ? (int)((TAPP >> (4 * T)) & 15) * cinb + c * 128 : ncn * 128;
         if (!(ab & 4)) load_w(kbn, wnxt);
         if (!(ab & 2)) {
 #pragma unroll
           for (int e = 0; e < 3; ++e) {
-            const int d = SCH[T][e];
-            if (d >= 0) {  // uniform
+            const uint64_t sp = e == 0 ? SCHP0 : e == 1 ? SCHP1 : SCHP2;
+            const int d = (int)((sp >> (7 * T)) & 0x7F);
+            if (d != 0x7F) {  // uniform
               const bool nx = (d >> 2) & 1;
-              issue(d & 3, nx ? nt : t, nx ? ncn : c, d >> 3);
+              issue(d & 3, nx ? tn : tcur, nx ? ncn : c, d >> 3);
             }
           }
         }
-        step(OFF[TPL[T]] + TRO[T] * PITCH, TCO[T]);
+        const int sd = (int)((STEPP >> (4 * T)) & 15), pl = sd & 3;
+        int co;  // opaque: a known 0/1 index turns step()'s select into a scratch-array load
+        asm volatile("s_lshr_b32 %0, %1, 3" : "=s"(co) : "s"(sd));
+        step(1024 * (37 * pl - (pl == 3 ? 3 : 0)) + ((sd >> 2) & 1) * PITCH, co);
       }
     }
     if (!(ab & 8)) epilogue(t);

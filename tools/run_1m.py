@@ -46,14 +46,14 @@ def main(argv=None, return_logits: bool = False):
     ap.add_argument('--chunk', type=int, default=4096, help='segments per device batch')
     ap.add_argument('--heads', type=int, default=6)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'bf16x3', 'fp32'])
-    ap.add_argument('--micro-batch', type=int, default=0, help='0: 1024 bf16, 256 bf16x3, 128 fp32')
+    ap.add_argument('--micro-batch', type=int, default=0, help='0: 2048 bf16, 512 bf16x3, 128 fp32 (as bench.py)')
     ap.add_argument('--host-fed', action='store_true', help='PCM from pinned host memory (H2D inside the timing)')
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'], help='gloo: tests only')
     ap.add_argument('--one-device', action='store_true', help='every rank on cuda:0 (2-rank test on one GPU)')
     ap.add_argument('--out-logits', default='', help='rank 0 saves the gathered logits here (tests)')
     args = ap.parse_args(argv)
-    args.micro_batch = args.micro_batch or {'bf16': 1024, 'bf16x3': 256, 'fp32': 128}[args.dtype]
+    args.micro_batch = args.micro_batch or {'bf16': 2048, 'bf16x3': 512, 'fp32': 128}[args.dtype]
 
     from sad import launch
     if args.gpus > 1 and not launch.under_launcher():
