@@ -219,9 +219,13 @@ class Mode:
     (Round 4 ran the next step's front end on a side stream during this step's
     backbone, +0.9 %.  Round 5's repeated hand-off test found the backbone
     reading stale map lines in a fraction of the steps on this runtime, with
-    event waits, host waits or an explicit L2 invalidate on every XCD
-    (tools/overlap_repeat*.py), so every stage of a step now
-    runs on the one stream.)"""
+    event waits or host waits (tools/handoff_study.py), so every
+    stage of a step runs on the one stream.)
+
+    After the timed steps, ``run`` checks the LAST timed step's outputs: its
+    merged logits must equal an untimed sequential forward of the same PCM bit
+    for bit, and with N > 1 every rank's gathered logits must hold each rank's
+    merged rows (``timed_output_check``; a mismatch raises)."""
 
     def __init__(self, sd, dev, dtype, micro_batch, B, world):
         from sad.engine import Engine
@@ -290,7 +294,35 @@ class Mode:
             r['rank_gather_ms'] = [round(x[1].item(), 4) for x in allt]
         r['ms'] = r['elapsed'] * 1e3 / steps
         r['value'] = self.world * self.B * steps / r['elapsed']
+        r['timed_output_check'] = self.check_outputs(pcm)
         return r
+
+    def check_outputs(self, pcm):
+        """The last timed step's outputs against an untimed sequential forward
+        (outside the timed region).  Raises on any difference."""
+        last = self.merged.clone()
+        _, ref = self.eng.forward_pcm(pcm)
+        torch.cuda.synchronize()
+        same = torch.equal(last, ref)
+        chk = {'what': 'last timed step merged logits vs an untimed sequential forward of the same PCM, bit for bit',
+               'bit_identical': same, 'max_abs_diff': (last - ref).abs().max().item()}
+        if self.gathered is not None:
+            rank = dist.get_rank()
+            own = torch.equal(self.gathered.chunk(self.world)[rank], last)
+            # every rank's gathered tensor must be the same bytes: compare a sum of its int32 words
+            h = self.gathered.view(torch.int32).to(torch.int64).sum().reshape(1)
+            hs = [torch.empty_like(h) for _ in range(self.world)]
+            dist.all_gather(hs, h)
+            ok = torch.tensor([int(own and same and len({int(x.item()) for x in hs}) == 1)], device=self.dev)
+            oks = [torch.empty_like(ok) for _ in range(self.world)]
+            dist.all_gather(oks, ok)
+            chk['gathered_holds_own_rows'] = own
+            chk['gathered_identical_on_all_ranks'] = len({int(x.item()) for x in hs}) == 1
+            chk['all_ranks_ok'] = all(int(x.item()) == 1 for x in oks)
+            same = chk['all_ranks_ok']
+        if not same:
+            raise RuntimeError(f'timed step outputs differ from the sequential forward: {chk}')
+        return chk
 
 
 def kernel_roofline(r, mfma_factor=1):
@@ -455,6 +487,7 @@ def main():
                                       'achieved_gbps': round(FE_BYTES * B / (r['fe_ms'] * 1e-3) / 1e9, 1),
                                       'segments_per_s': round(B / (r['fe_ms'] * 1e-3), 1)}},
             'accuracy': accuracy(head),
+            'timed_output_check': r['timed_output_check'],
         }
         if par is not None:
             palg, pexe, pinfo = kernel_roofline(par, 3)
@@ -478,7 +511,8 @@ def main():
                                                                   1),
                              'backbone_executed_frac': round(3 * BACKBONE_FLOP * B / (par['bb_ms'] * 1e-3) / 1e12
                                                              / BF16_PEAK_TFLOPS, 4)},
-                'accuracy': accuracy(par_mode) if par_mode is not head else out['accuracy']}
+                'accuracy': accuracy(par_mode) if par_mode is not head else out['accuracy'],
+                'timed_output_check': par['timed_output_check']}
         if world == 1 and args.fp32_steps > 0 and args.dtype != 'fp32':
             f = Mode(sd, dev, 'fp32', mbs['fp32'], B, 1).run(pcm, args.fp32_steps, 1, profile=False)
             out['fp32_mode'] = {'value': round(f['value'], 1), 'unit': 'segments/s', 'ms_per_step': round(f['ms'], 3),

@@ -22,7 +22,14 @@
  *     sad_frontend_run);
  *   - *_run calls are asynchronous on the given hipStream_t (passed as void*),
  *     never allocate, never synchronise (graph-capturable);
- *   - distinct plans / streams may be used from different threads.
+ *   - distinct plans / streams may be used from different threads;
+ *   - cross-stream hand-offs need only the usual event: an output written on
+ *     one stream (a libsad call, or a collective on the NCCL/RCCL stream) may
+ *     be consumed by a *_run on another stream after hipStreamWaitEvent (or a
+ *     host wait) on an event recorded after the producer.  Kernels of
+ *     different streams may run concurrently and co-reside on a CU; the
+ *     outputs do not depend on it (tests/test_gpu_handoff.py: the front end
+ *     beside the stem, and heads / AdamW / backbone fed from a side stream).
  */
 #ifndef SAD_H_
 #define SAD_H_

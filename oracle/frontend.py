@@ -152,9 +152,9 @@ def batch_maps(pcm_i16, sr: int = 32000, cfg: SpectrogramConfig | None = None, d
 
     Each segment goes through the reference's per-window path separately (the
     top-db clamp and the moments are per segment).
-    dtype float64 gives the same arithmetic without the fp32 rounding (the
-    filterbank too): what the tests measure both the device and the fp32
-    restatement against."""
+    dtype float64 runs the STFT, projection and dB arithmetic without fp32
+    rounding; the filterbank stays torchaudio's fp32 bank (melscale_fbanks),
+    only cast, as mel_spectrogram does with fb.to(spec.dtype)."""
     t = torch.as_tensor(pcm_i16)
     dbs, maps = [], []
     for i in range(t.shape[0]):

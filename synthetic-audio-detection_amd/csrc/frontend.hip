@@ -385,7 +385,18 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     }
     wave_lds_sync();
     // ---- real-spectrum recovery + power for bins [bin_lo, bin_hi]
-    for (int k = bin_lo + lane; k <= bin_hi; k += 64) {
+    // Every lane runs the same trip count (the last round's surplus lanes
+    // compute a clamped bin and do not store it).  With `k <= bin_hi` as the
+    // loop bound, lane 63 had one bin fewer than the others (767 bins), and the
+    // compiler's pairwise-vectorised loop left that lane's last bin to a
+    // one-active-lane remainder loop; while the backbone's stem ran on another
+    // stream, that single-lane packed-FP32 sequence stored a power off by ~1e-3
+    // relative in about one frame in 10^6 (bin 705 = mel rows 124/125,
+    // tools/fe_concurrency.py).
+    const int n_kit = (bin_hi - bin_lo + 64) / 64;
+    for (int it = 0; it < n_kit; ++it) {
+      const int k_raw = bin_lo + lane + 64 * it;
+      const int k = k_raw <= bin_hi ? k_raw : bin_hi;
       const float2 A = buf[fe_zslot(k & (FE_NC - 1))];
       const float2 Bc = buf[fe_zslot((FE_NC - k) & (FE_NC - 1))];
       const float2 B = make_float2(Bc.x, -Bc.y);              // conj(Z[N/2-k])
@@ -398,7 +409,7 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
       if (k & 1) w2 = cmul(w2, make_float2(0.99999529380957619f, -0.0030679567629659761f));
       const float2 WO = cmul(w2, O);
       const float re = E.x + WO.x, im = E.y + WO.y;
-      pw[k - bin_lo + FE_PWPAD] = re * re + im * im;
+      if (k_raw <= bin_hi) pw[k - bin_lo + FE_PWPAD] = re * re + im * im;
     }
     wave_lds_sync();
     if (staged) {
@@ -635,6 +646,17 @@ using namespace sad;
 struct sad_frontend_plan : sad::FrontendPlan {};
 
 // fb: [n_fft / 2 + 1][n_mels] fp32, the mel filterbank the plan projects on
+// SAD_FE_FUSED: 0 the two-kernel form (fe_mel_db + fe_normalize); 1 fused,
+// agent-scope release / acquire fences; 2 fused, the tiles stored and re-read
+// at agent scope (sc1) with no cache write-back / invalidate
+static int fe_fused() {
+  static const int v = [] {
+    const char* e = getenv("SAD_FE_FUSED");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 static int frontend_plan_build(const sad_frontend_cfg* cfg, const float* fb_in, sad_frontend_plan** out) {
   SAD_REQUIRE(cfg && out, "null cfg/out");
   SAD_REQUIRE(cfg->n_fft == FE_NFFT, "only n_fft = 2048 is supported");
@@ -792,8 +814,11 @@ static int frontend_plan_build(const sad_frontend_cfg* cfg, const float* fb_in, 
   if (lanes_ok) {
     UP(p->d_lane_tab, lane_tab);
     UP(p->d_lane_w, lane_w);
-    // the fused normalisation's counters (zero; each launch leaves them zero)
-    // and block maxima, for one launch chunk
+  }
+  if (lanes_ok && fe_fused()) {
+    // only the one-kernel form (SAD_FE_FUSED=1/2, off by default) needs the
+    // fused normalisation's counters (zero; each launch leaves them zero) and
+    // block maxima, for one launch chunk; the default plan stays immutable
     const int n_fb = (p->n_frames + FE_FRAMES_PER_WG - 1) / FE_FRAMES_PER_WG;
     std::vector<unsigned> zeros(FE_CHUNK, 0u);
     UP(p->d_seg_cnt, zeros);
@@ -834,17 +859,6 @@ extern "C" int sad_frontend_frames(const sad_frontend_plan* p, int32_t* n) {
   SAD_REQUIRE(p && n, "null");
   *n = p->n_frames;
   return SAD_OK;
-}
-
-// SAD_FE_FUSED: 0 the two-kernel form (fe_mel_db + fe_normalize); 1 fused,
-// agent-scope release / acquire fences; 2 fused, the tiles stored and re-read
-// at agent scope (sc1) with no cache write-back / invalidate
-static int fe_fused() {
-  static const int v = [] {
-    const char* e = getenv("SAD_FE_FUSED");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
 }
 
 // SAD_FE_XCD_MAP=1: the XCD-aware block order (a segment's blocks on one XCD)

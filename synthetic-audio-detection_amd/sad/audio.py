@@ -142,10 +142,10 @@ def melscale_fbanks(n_freqs: int, f_min: float, f_max: float, n_mels: int, sampl
     slaney area norm evaluated in torch fp32 arithmetic, op for op, so the
     weights are torchaudio's to the bit.  Plan-time data for
     sad_frontend_plan_create_fb (the device projects on these weights)."""
-    hz = torch.linspace(0, sample_rate // 2, n_freqs)  # fp32, torch's linspace
+    hz = torch.linspace(0, sample_rate // 2, n_freqs, dtype=torch.float32)  # fp32 whatever the default dtype
     mel_lo = 2595.0 * math.log10(1.0 + f_min / 700.0)  # python float64 scalars
     mel_hi = 2595.0 * math.log10(1.0 + f_max / 700.0)
-    pts = 700.0 * (10.0 ** (torch.linspace(mel_lo, mel_hi, n_mels + 2) / 2595.0) - 1.0)
+    pts = 700.0 * (10.0 ** (torch.linspace(mel_lo, mel_hi, n_mels + 2, dtype=torch.float32) / 2595.0) - 1.0)
     gaps = pts[1:] - pts[:-1]
     rel = pts.unsqueeze(0) - hz.unsqueeze(1)                 # [n_freqs, n_mels + 2]
     rising = (-1.0 * rel[:, :-2]) / gaps[:-1]

@@ -94,6 +94,8 @@ class FrontEnd:
         from .audio import melscale_fbanks
         fb = melscale_fbanks(n_fft // 2 + 1, float(f_min), float(f_max), n_mels, sample_rate,
                              norm == 'slaney').contiguous()
+        # the plan reads a host fp32 [n_freqs, n_mels] array through this pointer
+        assert fb.dtype == torch.float32 and fb.device.type == 'cpu' and fb.is_contiguous()
         with torch.cuda.device(self.device):
             _lib.call('sad_frontend_plan_create_fb', _lib.ctypes.byref(cfg), fb.data_ptr(),
                       _lib.ctypes.byref(self._plan))

