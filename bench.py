@@ -214,20 +214,22 @@ def ingest_leg(eng, dev, minutes: float = 2.0, reps: int = 3):
 
 class Mode:
     """One engine configuration timed on this rank's resident PCM: each step is
-    front end -> backbone -> heads (-> all-gather) on the current stream.
+    front end -> backbone -> heads (-> all-gather).
 
-    (Round 4 ran the next step's front end on a side stream during this step's
-    backbone, +0.9 %.  Round 5's repeated hand-off test found the backbone
-    reading stale map lines in a fraction of the steps on this runtime, with
-    event waits or host waits (tools/handoff_study.py), so every
-    stage of a step runs on the one stream.)
+    overlap: the next step's front end runs on a side stream while this step's
+    backbone runs (two map slots; every step still takes its whole batch
+    through every stage, the front end just starts one step early).  Round 5
+    withdrew this after wrong logits in some pipelined steps; round 6 traced
+    them to the front end computing one power bin wrongly when it shared CUs
+    with the stem (a one-active-lane loop remainder, fixed in frontend.hip;
+    DESIGN.md 5c, tests/test_gpu_handoff.py), not to the hand-off.
 
     After the timed steps, ``run`` checks the LAST timed step's outputs: its
     merged logits must equal an untimed sequential forward of the same PCM bit
     for bit, and with N > 1 every rank's gathered logits must hold each rank's
     merged rows (``timed_output_check``; a mismatch raises)."""
 
-    def __init__(self, sd, dev, dtype, micro_batch, B, world):
+    def __init__(self, sd, dev, dtype, micro_batch, B, world, overlap=False):
         from sad.engine import Engine
         self.eng = Engine(sd, dev, dtype=dtype, micro_batch=micro_batch)
         self.dtype, self.mb, self.B, self.world, self.dev = dtype, micro_batch, B, world, dev
@@ -235,14 +237,38 @@ class Mode:
         self.logits = torch.empty(B, HEADS, 2, device=dev)
         self.merged = torch.empty(B, HEADS + 1, device=dev)
         self.gathered = torch.empty(world * B, HEADS + 1, device=dev) if world > 1 else None
+        self.overlap = overlap
+        if overlap:
+            self.side = torch.cuda.Stream(dev)
+            self.maps = [torch.empty(B, 128, 251, device=dev) for _ in range(2)]
+            self.fe_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self.bb_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self.i = 0
+
+    def _frontend_ahead(self, pcm, slot):
+        # the slot's previous reader (the backbone two steps back) must be done
+        self.side.wait_event(self.bb_done[slot])
+        with torch.cuda.stream(self.side):
+            self.eng.frontend(pcm, out=self.maps[slot])
+        self.fe_done[slot].record(self.side)
 
     def step(self, pcm, ev=None):
         if ev is not None:
             ev[0].record()
-        m = self.eng.frontend(pcm)
+        if self.overlap:  # this step's maps were computed during the previous step (the bench repeats one batch)
+            slot = self.i & 1
+            if self.i == 0:
+                self._frontend_ahead(pcm, slot)
+            cur = torch.cuda.current_stream()
+            cur.wait_event(self.fe_done[slot])
+            m = self.maps[slot]
+        else:
+            m = self.eng.frontend(pcm)
         if ev is not None:
             ev[1].record()
         self.eng.backbones[0](m, out=self.feats)
+        if self.overlap:
+            self.bb_done[slot].record(cur)
         if ev is not None:
             ev[2].record()
         self.eng.heads([self.feats], self.logits, self.merged)
@@ -255,6 +281,28 @@ class Mode:
                 dist.all_gather(list(self.gathered.chunk(self.world)), self.merged)
         if ev is not None:
             ev[4].record()
+        if self.overlap:  # the next step's front end, during this step's backbone
+            self._frontend_ahead(pcm, slot ^ 1)
+            self.i += 1
+
+    def isolated(self, pcm, reps=5):
+        """Front end and backbone timed alone (HIP events on the current
+        stream, best of reps): the per-stage rooflines of an overlapped run,
+        whose concurrent stages stretch each other."""
+        cur = torch.cuda.current_stream()
+        torch.cuda.synchronize()
+        fe, bb = [], []
+        for _ in range(reps):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record(cur)
+            m = self.eng.frontend(pcm)
+            e[1].record(cur)
+            self.eng.backbones[0](m, out=self.feats)
+            e[2].record(cur)
+            torch.cuda.synchronize()
+            fe.append(e[0].elapsed_time(e[1]))
+            bb.append(e[1].elapsed_time(e[2]))
+        return min(fe), min(bb)
 
     def run(self, pcm, steps, warmup, profile=True):
         from sad import _lib
@@ -295,6 +343,11 @@ class Mode:
         r['ms'] = r['elapsed'] * 1e3 / steps
         r['value'] = self.world * self.B * steps / r['elapsed']
         r['timed_output_check'] = self.check_outputs(pcm)
+        if self.overlap:
+            # the stage rooflines from the stages run alone; the in-step events
+            # bracket the wait for the side stream's front end, not its work
+            r['fe_ms_in_step'], r['bb_ms_in_step'] = r['fe_ms'], r['bb_ms']
+            r['fe_ms'], r['bb_ms'] = self.isolated(pcm)
         return r
 
     def check_outputs(self, pcm):
@@ -376,6 +429,8 @@ def main():
     ap.add_argument('--parity-steps', type=int, default=0, help='timed steps of the bf16x3 parity mode '
                                                                 '(0: max(steps // 3, 3); -1: skip)')
     ap.add_argument('--fp32-steps', type=int, default=2, help='timed steps of the fp32 mode (N = 1; 0: skip)')
+    ap.add_argument('--overlap-frontend', type=int, default=1,
+                    help="1: each step's front end runs on a side stream during the previous step's backbone")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--kernels-only', action='store_true',
                     help='profiling runs: only the headline mode (no parity/fp32 legs, accuracy or CPU baseline)')
@@ -404,7 +459,8 @@ def main():
     pcm = torch.empty(B, SEG, dtype=torch.int16, device=dev)
     _lib.call('sad_synth_pcm', 0, rank * B, B, SEG, _lib.ptr(pcm), _lib.stream_handle(dev))
 
-    head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world)
+    ov = bool(args.overlap_frontend)
+    head = Mode(sd, dev, args.dtype, args.micro_batch or mbs[args.dtype], B, world, overlap=ov)
     r = head.run(pcm, args.steps, args.warmup)
     p_steps = max(args.steps // 3, 3) if args.parity_steps == 0 else args.parity_steps
     if args.kernels_only:
@@ -414,7 +470,7 @@ def main():
         if args.dtype == 'bf16x3':
             par_mode, par = head, r
         else:
-            par_mode = Mode(sd, dev, 'bf16x3', mbs['bf16x3'], B, world)
+            par_mode = Mode(sd, dev, 'bf16x3', mbs['bf16x3'], B, world, overlap=ov)
             par = par_mode.run(pcm, p_steps, 1)
 
     if rank == 0:
@@ -467,6 +523,7 @@ def main():
                                    '-> ResNet-18@512x512 -> 6 binary heads -> merge (+RCCL all-gather of logits)',
                        'segments_per_gpu_per_step': B, 'heads': HEADS, 'distinct_backbones': 1,
                        'micro_batch': head.mb, 'parallelism': f'dp{world}',
+                       'frontend_overlapped': ov,
                        'per_rank_ms_per_step': r['rank_ms_per_step'], 'per_rank_allgather_ms': r['rank_gather_ms']},
             'roofline': {'bound': 'mfma',
                          'kernel': DOMINANT[args.dtype][2],

@@ -6,6 +6,11 @@ layer4 backward + RCCL all-reduce of the gradients + clip + AdamW -- on 1..8
 MI355X, one process per GPU: under torchrun, or started bare with --gpus N,
 in which case it starts the N ranks itself (sad/launch.py, like bench.py).
 
+``--head-loss`` trains through model.head (submodel_trainer.py --head-loss):
+CE and both accuracies on the BinaryClassifier's two logits; by default they
+run on the 512 pooled features as in the reference (quirk C1), where the
+eval accuracy of a two-class problem says little.
+
 Workload per rank and step: ``--batch-size`` files (default 32, the reference
 default) x 2 segments = 64 segments of synthetic labelled audio
 (sad.synth.synth_labelled_clip: class 1 = noise + harmonic stack, class 0 =
@@ -40,6 +45,9 @@ def main():
     ap.add_argument('--pool', type=int, default=256, help='synthetic training clips per rank')
     ap.add_argument('--eval-clips', type=int, default=64)
     ap.add_argument('--lr', type=float, default=1e-3)
+    ap.add_argument('--head-loss', action='store_true',
+                    help="submodel_trainer.py --head-loss: CE / accuracy on model.head's 2 logits (default: the "
+                         "reference's pooled features, quirk C1)")
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'], help='gloo: tests only')
     ap.add_argument('--one-device', action='store_true', help='every rank on cuda:0 (2-rank test on one GPU)')
     args = ap.parse_args()
@@ -63,7 +71,7 @@ def main():
     from sad.synth import synth_labelled_clip
     torch.manual_seed(42)
     base, head = st.init_state_dict(42)
-    tr = st.Trainer(base, head, dev, args.dtype, lr=args.lr, group=group, world=world)
+    tr = st.Trainer(base, head, dev, args.dtype, lr=args.lr, group=group, world=world, head_loss=args.head_loss)
     fe = st.TrainFrontEnd(dev, args.dtype)
     P = args.pool
     labels = np.arange(P) % 2
@@ -123,6 +131,8 @@ def main():
     ev = torch.from_numpy(np.stack([synth_labelled_clip(10_000 + rank, i, int(el[i]))[:128000]
                                     for i in range(E)]).astype(np.float32) / 32768.0).to(dev)
     feats = bb(fe.maps(ev))
+    if args.head_loss:
+        feats = tr.net.head_forward(feats, train=False)
     _, lc = st.ce_loss(feats, torch.from_numpy(el).long())
     eval_correct = lc[1].item()
     if world > 1:
@@ -141,6 +151,7 @@ def main():
             'config': {'workload': 'train step: front end + train-mode ResNet-18 fwd + CE + layer4 bwd + '
                                    'all-reduce + clip + AdamW', 'files_per_gpu': B, 'segments_per_gpu': 2 * B,
                        'parallelism': f'dp{world}'},
+            'head_loss': args.head_loss,
             'train_loss_first_last': [round(losses[0], 4), round(losses[-1], 4)],
             'train_accuracy_timed_steps': round(100.0 * correct / max(rows, 1), 2),
             'eval_accuracy_after': round(100.0 * eval_correct / E, 2),

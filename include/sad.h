@@ -410,6 +410,32 @@ int sad_bn_relu_maxpool_run(const void* x, int64_t n, int32_t H, int32_t W, int3
  * argmax (first maximum, outputs.max(1) at :281,346). */
 int sad_ce_loss_run(const float* logits, const int64_t* target, int64_t B, int32_t C, float scale, float* dlogits,
                     float* out, int32_t* pred, void* stream);
+/* The BinaryClassifier head in train mode (optional --head-loss of
+ * submodel_trainer.py; the reference builds it at :613-625 and never calls it,
+ * quirk C1): Linear(nf,512) -> BatchNorm1d(512) -> ReLU -> Dropout(p1) ->
+ * Linear(512,256) -> BatchNorm1d(256) -> ReLU -> Dropout(p2) -> Linear(256,2).
+ * Parameters are the head.* tensors (nn.Sequential indices 2, 3, 6, 7, 10),
+ * fp32, device.  Dropout keeps element i of layer L (1, 2) when
+ * u(seed, L, i) >= p, u from a splitmix64 hash (headtrain.hip hkeep), so the
+ * backward regenerates the forward's masks from the same seed. */
+typedef struct {
+  const float *w2, *b2, *g3, *be3, *w6, *b6, *g7, *be7, *w10, *b10;
+  float *rm3, *rv3, *rm7, *rv7; /* BN running statistics (updated in train mode) */
+  int32_t in_features;          /* the backbone's num_features (512 / 2048) */
+  float eps, momentum, p1, p2;  /* 1e-5, 0.1, 0.5, 0.3 in the reference */
+} sad_head_params;
+int sad_head_workspace_size(int64_t B, int32_t in_features, size_t* bytes);
+/* feats [B, nf] -> logits [B, 2].  train: batch statistics (running stats
+ * updated) and dropout; 0: eval (running stats, no dropout).  ws keeps the
+ * activations the backward needs. */
+int sad_head_train_forward_run(const sad_head_params* h, const float* feats, int64_t B, int32_t train, uint64_t seed,
+                               float* logits, void* ws, size_t ws_bytes, void* stream);
+/* After a train-mode forward with the same feats / seed / ws: dlogits [B, 2]
+ * -> dfeats [B, nf] and grads = the head's parameter gradients, flat fp32 in
+ * parameters() order (2.w, 2.b, 3.w, 3.b, 6.w, 6.b, 7.w, 7.b, 10.w, 10.b). */
+int sad_head_train_backward_run(const sad_head_params* h, const float* feats, int64_t B, uint64_t seed,
+                                const float* dlogits, float* dfeats, float* grads, void* ws, size_t ws_bytes,
+                                void* stream);
 /* BatchNorm2d train-mode backward through an optional ReLU:
  * dz = (dy | dpool[n][c]/pool_hw broadcast) * [y > 0 if y];  dbeta = sum dz,
  * dgamma = sum dz*xhat (written, or added if accumulate);  dx = gamma*invstd*

@@ -95,3 +95,54 @@ def train_step(model: TrainModel, opt, inputs: torch.Tensor, targets: torch.Tens
     norm = torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=0.5)
     opt.step()
     return loss.detach(), outputs.detach(), norm
+
+
+# --------------------------------------------------------------- --head-loss
+# The reference's model.head (submodel_trainer.py:613-625) in train mode, for
+# the drop-in's optional --head-loss path (sad_head_train_*_run): the pooled
+# features -> Linear -> BatchNorm1d (batch statistics) -> ReLU -> Dropout ->
+# Linear -> BatchNorm1d -> ReLU -> Dropout -> Linear.  torch's dropout draws
+# its masks from its own generator; the device draws them from a counter hash,
+# restated here so the oracle can apply the same masks (parity of everything
+# else is then exact arithmetic).
+HEAD_DROPOUT = (0.5, 0.3)
+
+
+def head_keep_mask(seed: int, layer: int, rows: int, cols: int, p: float):
+    """bool [rows, cols]: element i = r * cols + c of dropout layer `layer`
+    (1, 2) is kept when u >= p, u = (splitmix64(seed + golden * (i + 1) +
+    layer << 56) >> 40) / 2^24 (csrc/headtrain.hip hkeep)."""
+    import numpy as np
+    M = (1 << 64) - 1
+    with np.errstate(over='ignore'):
+        i = np.arange(rows * cols, dtype=np.uint64)
+        z = (np.uint64(seed & M) + np.uint64(0x9E3779B97F4A7C15) * (i + np.uint64(1))
+             + np.uint64((layer << 56) & M))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    u = (z >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return torch.from_numpy((u >= np.float32(p)).reshape(rows, cols))
+
+
+def head_module(head_sd: dict, num_features: int = 512) -> nn.Sequential:
+    """model.head[2:] with the given state (keys '2.weight', ..., nn.Sequential
+    indices of :613-625), as plain torch modules; dropout is applied by
+    head_forward with explicit masks."""
+    m = nn.Sequential(nn.Identity(), nn.Identity(), nn.Linear(num_features, 512), nn.BatchNorm1d(512), nn.ReLU(),
+                      nn.Identity(), nn.Linear(512, 256), nn.BatchNorm1d(256), nn.ReLU(), nn.Identity(),
+                      nn.Linear(256, 2))
+    m.load_state_dict({k: torch.as_tensor(v) for k, v in head_sd.items()}, strict=True)
+    return m
+
+
+def head_forward(m: nn.Sequential, feats: torch.Tensor, train: bool, seed: int = 0) -> torch.Tensor:
+    """The head on pooled features [B, nf]; train mode with the device's masks."""
+    m.train(train)
+    x = m[4](m[3](m[2](feats)))
+    if train:
+        x = x * head_keep_mask(seed, 1, *x.shape, HEAD_DROPOUT[0]) / (1 - HEAD_DROPOUT[0])
+    x = m[8](m[7](m[6](x)))
+    if train:
+        x = x * head_keep_mask(seed, 2, *x.shape, HEAD_DROPOUT[1]) / (1 - HEAD_DROPOUT[1])
+    return m[10](x)

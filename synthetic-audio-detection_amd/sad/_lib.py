@@ -45,6 +45,14 @@ class PackSeg(ctypes.Structure):
                 ('mode0', P), ('mode1', P)]
 
 
+class HeadParams(ctypes.Structure):
+    """sad_head_params (include/sad.h): the train-mode head's device tensors."""
+    _fields_ = [(n, P) for n in ('w2', 'b2', 'g3', 'be3', 'w6', 'b6', 'g7', 'be7', 'w10', 'b10',
+                                 'rm3', 'rv3', 'rm7', 'rv7')] + \
+               [('in_features', I32), ('eps', ctypes.c_float), ('momentum', ctypes.c_float),
+                ('p1', ctypes.c_float), ('p2', ctypes.c_float)]
+
+
 SIGNATURES = {
     'sad_init': (ctypes.c_int, [ctypes.c_int]),
     'sad_shutdown': (ctypes.c_int, []),
@@ -119,6 +127,11 @@ SIGNATURES = {
     'sad_conv_dgrad_run': (ctypes.c_int, [P, I64, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32, P, P,
                                           SZ, P]),
     'sad_clip_grad_norm_run': (ctypes.c_int, [P, I64, ctypes.c_float, P, P, SZ, P]),
+    'sad_head_workspace_size': (ctypes.c_int, [I64, I32, ctypes.POINTER(SZ)]),
+    'sad_head_train_forward_run': (ctypes.c_int, [ctypes.POINTER(HeadParams), P, I64, I32, ctypes.c_uint64, P, P,
+                                                  SZ, P]),
+    'sad_head_train_backward_run': (ctypes.c_int, [ctypes.POINTER(HeadParams), P, I64, ctypes.c_uint64, P, P, P,
+                                                   P, SZ, P]),
     'sad_adamw_run': (ctypes.c_int, [P, P, P, P, I64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                      ctypes.c_float, ctypes.c_float, I64, P]),
     'sad_adamw_pack_run': (ctypes.c_int, [P, P, P, P, I64, ctypes.c_float, ctypes.c_float, ctypes.c_float,

@@ -109,6 +109,21 @@ def head_keys():
     return keys
 
 
+# BinaryClassifier head in train mode (--head-loss): Dropout rates of the
+# reference's model.head (submodel_trainer.py:613-625)
+HEAD_DROPOUT = (0.5, 0.3)
+
+
+def head_param_layout(num_features: int = 512):
+    """[(name, shape)] of model.head's parameters in ``parameters()`` order
+    (nn.Sequential indices 2, 3, 6, 7, 10): the layout of
+    sad_head_train_backward_run's gradient buffer."""
+    out = []
+    for idx, kind, shape in head_layout(num_features):
+        out += [(f'head.{idx}.weight', shape), (f'head.{idx}.bias', (shape[0],))]
+    return out
+
+
 # --------------------------------------------------------------- initialisation
 def init_state_dict(seed: int = 42, model_name: str = 'resnet18'):
     """Initial trainer model, ``torch.manual_seed(seed)`` then
@@ -205,7 +220,7 @@ class TrainNet:
     """timm resnet18 / resnet34 (+ the unused MLP head) in train mode on one device."""
 
     def __init__(self, base_sd: Dict[str, torch.Tensor], head_sd: Dict[str, torch.Tensor], device='cuda',
-                 dtype: str = 'bf16', model_name: str = 'resnet18'):
+                 dtype: str = 'bf16', model_name: str = 'resnet18', head_loss: bool = False):
         self.device = _dev(device)
         self.model_name = model_name
         self.bottleneck, self.blocks, self.num_features = _blocks(model_name)
@@ -214,6 +229,12 @@ class TrainNet:
         self.tdtype = torch.bfloat16 if dtype == 'bf16' else torch.float32
         self.es = 2 if dtype == 'bf16' else 4
         layout = param_layout(model_name)
+        # --head-loss: the head's parameters follow the backbone's in the flat
+        # buffers (parameters() order), so the layer4 range's all-reduce, clip
+        # and AdamW cover them as the reference's optimizer does (:648-652)
+        self.head_loss = head_loss
+        if head_loss:
+            layout = layout + head_param_layout(self.num_features)
         self.names = [n for n, _ in layout]
         sizes = [int(np.prod(s)) for _, s in layout]
         offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
@@ -225,7 +246,8 @@ class TrainNet:
         for (n, s), (a, b) in zip(layout, [self.offsets[n] for n in self.names]):
             self.params[n] = self.pflat[a:b].view(s)
             self.grads[n] = self.gflat[a:b].view(s)
-            self.params[n].copy_(torch.as_tensor(base_sd[n], dtype=torch.float32))
+            src = head_sd[n[5:]] if n.startswith('head.') else base_sd[n]
+            self.params[n].copy_(torch.as_tensor(src, dtype=torch.float32))
         self.bn_keys = [k for k, _, kind in arch_param_shapes(model_name) if kind == 'bn']
         self.running = {}
         self.nbt = {}
@@ -234,6 +256,12 @@ class TrainNet:
                                torch.as_tensor(base_sd[f'{k}.running_var'], dtype=torch.float32).to(self.device).clone())
             self.nbt[k] = int(torch.as_tensor(base_sd.get(f'{k}.num_batches_tracked', 0)).item())
         self.head_sd = OrderedDict((k, torch.as_tensor(head_sd[k]).detach().clone().cpu()) for k in head_keys())
+        if head_loss:  # the head's BN running statistics live on the device while it trains
+            self.head_running = {i: tuple(torch.as_tensor(head_sd[f'{i}.{b}'], dtype=torch.float32).to(self.device)
+                                          .clone() for b in ('running_mean', 'running_var')) for i in (3, 7)}
+            self.head_nbt = {i: int(torch.as_tensor(head_sd.get(f'{i}.num_batches_tracked', 0)).item())
+                             for i in (3, 7)}
+            self.range_head = self.offsets['head.2.weight'][0], total
         self.range4 = (self.offsets['layer4.0.conv1.weight'][0], total)
         self.range3 = (self.offsets['layer3.0.conv1.weight'][0], self.range4[0])
         self.zero_bias = torch.zeros(max(FEATURES, self.num_features), device=self.device, dtype=torch.float32)
@@ -577,6 +605,62 @@ class TrainNet:
                       _lib.ptr(ws), ws.numel(), self._stream())
         return nc
 
+    # ---------------------------------------------------------- --head-loss
+    def _head_params(self) -> _lib.HeadParams:
+        p, (rm3, rv3), (rm7, rv7) = self.params, self.head_running[3], self.head_running[7]
+        t = [p[f'head.{i}.{w}'] for i in (2, 3, 6, 7, 10) for w in ('weight', 'bias')] + [rm3, rv3, rm7, rv7]
+        return _lib.HeadParams(*[x.data_ptr() for x in t], self.num_features, BN_EPS, BN_MOMENTUM, *HEAD_DROPOUT)
+
+    def head_forward(self, feats: torch.Tensor, train: bool = True, seed: int = 0) -> torch.Tensor:
+        """model.head on the pooled features (sad_head_train_forward_run): train
+        mode = batch-statistics BN (running stats updated) + dropout masks of
+        ``seed``; eval = running stats, no dropout.  -> logits [B, 2] fp32."""
+        B = feats.shape[0]
+        sz = _lib.SZ()
+        _lib.call('sad_head_workspace_size', B, self.num_features, _lib.ctypes.byref(sz))
+        ws = self._buf('head', sz.value)
+        logits = torch.empty(B, 2, device=self.device, dtype=torch.float32)
+        hp = self._head_params()
+        with torch.cuda.device(self.device):
+            _lib.call('sad_head_train_forward_run', _lib.ctypes.byref(hp), _lib.ptr(feats.contiguous()), B,
+                      int(train), seed & (2 ** 64 - 1), _lib.ptr(logits), _lib.ptr(ws), ws.numel(), self._stream())
+        if train:
+            for i in (3, 7):
+                self.head_nbt[i] += 1
+        return logits
+
+    def head_backward(self, feats: torch.Tensor, dlogits: torch.Tensor, seed: int = 0) -> torch.Tensor:
+        """After head_forward(train=True) with the same feats and seed: the head's
+        parameter gradients into gflat (overwritten) and d(loss)/d(feats)."""
+        B = feats.shape[0]
+        ws = self._ws['head']
+        dfeat = torch.empty(B, self.num_features, device=self.device, dtype=torch.float32)
+        a, b = self.range_head
+        hp = self._head_params()
+        with torch.cuda.device(self.device):
+            _lib.call('sad_head_train_backward_run', _lib.ctypes.byref(hp), _lib.ptr(feats.contiguous()), B,
+                      seed & (2 ** 64 - 1), _lib.ptr(dlogits.contiguous()), _lib.ptr(dfeat),
+                      _lib.ptr(self.gflat[a:b]), _lib.ptr(ws), ws.numel(), self._stream())
+        return dfeat
+
+    def current_head_sd(self) -> "OrderedDict[str, torch.Tensor]":
+        """model.head's state dict: the trained values under --head-loss, else
+        the untouched initial head (quirk C1)."""
+        if not self.head_loss:
+            return OrderedDict((k, v.clone()) for k, v in self.head_sd.items())
+        sd = OrderedDict()
+        for k in head_keys():
+            i, what = int(k.split('.')[0]), k.split('.', 1)[1]
+            if what in ('weight', 'bias'):
+                sd[k] = self.params[f'head.{k}'].detach().cpu().clone()
+            elif what == 'running_mean':
+                sd[k] = self.head_running[i][0].cpu().clone()
+            elif what == 'running_var':
+                sd[k] = self.head_running[i][1].cpu().clone()
+            else:
+                sd[k] = torch.tensor(self.head_nbt[i], dtype=torch.long)
+        return sd
+
     # ---------------------------------------------------------- eval / export
     def base_state_dict(self) -> "OrderedDict[str, torch.Tensor]":
         """timm-keyed backbone state dict (CPU), parameters + BN buffers."""
@@ -597,8 +681,8 @@ class TrainNet:
         """``get_model(model).state_dict()`` of the reference trainer: timm keys,
         then ``head.*`` (submodel_trainer.py:706)."""
         sd = self.base_state_dict()
-        for k, v in self.head_sd.items():
-            sd[f'head.{k}'] = v.clone()
+        for k, v in self.current_head_sd().items():
+            sd[f'head.{k}'] = v
         return sd
 
     def eval_backbone(self, micro_batch: int = 64):
@@ -625,8 +709,8 @@ class MixedNet(TrainNet):
     weights never change (layer3 is never stepped), so its fp32 packed copies
     stay valid.  Evaluation runs the split-bf16 inference plan (|dlogit| <= 1e-3)."""
 
-    def __init__(self, base_sd, head_sd, device='cuda', model_name: str = 'resnet18'):
-        super().__init__(base_sd, head_sd, device, 'bf16', model_name)
+    def __init__(self, base_sd, head_sd, device='cuda', model_name: str = 'resnet18', head_loss: bool = False):
+        super().__init__(base_sd, head_sd, device, 'bf16', model_name, head_loss)
         pre = TrainNet.__new__(TrainNet)
         pre.__dict__.update(self.__dict__)
         pre.dtype, pre._dt, pre.tdtype, pre.es = 'fp32', _lib.SAD_F32, torch.float32, 4
@@ -692,9 +776,19 @@ class Trainer:
     accumulator, with an optional process group (DDP over RCCL)."""
 
     def __init__(self, base_sd, head_sd, device='cuda', dtype: str = 'bf16', lr: float = 1e-3, group=None,
-                 world: int = 1, model_name: str = 'resnet18'):
-        self.net = (MixedNet(base_sd, head_sd, device, model_name) if dtype == 'mixed'
-                    else TrainNet(base_sd, head_sd, device, dtype, model_name))
+                 world: int = 1, model_name: str = 'resnet18', head_loss: bool = False, seed: int = 42):
+        """head_loss: CrossEntropy on model.head's two logits (train-mode head,
+        trained with layer4) instead of the reference's pooled features (quirk
+        C1, the default)."""
+        self.net = (MixedNet(base_sd, head_sd, device, model_name, head_loss) if dtype == 'mixed'
+                    else TrainNet(base_sd, head_sd, device, dtype, model_name, head_loss))
+        self.head_loss = head_loss
+        rank = 0
+        if world > 1:
+            import torch.distributed as dist
+            rank = dist.get_rank(group)
+        # dropout masks: one stream of counter-hash draws per (seed, rank); step k uses seed_base + k
+        self._seed_base = ((seed & 0xFFFFFFFF) << 24) ^ (rank << 56)
         self.device = self.net.device
         self.group, self.world = group, world
         a4, b4 = self.net.range4
@@ -711,6 +805,8 @@ class Trainer:
         # is never called (sad_adamw_run is the step).
         l4 = [n for n in self.net.names if n.startswith('layer4.')]
         self.l4_names = l4
+        # the optimizer's parameters in order: layer4, then the head (stepped only with head_loss)
+        self.opt_names = l4 + ([n for n in self.net.names if n.startswith('head.')] if head_loss else [])
         self._head_params = [torch.nn.Parameter(self.net.head_sd[k].clone().float())
                              for k in head_keys() if not k.endswith(('running_mean', 'running_var',
                                                                      'num_batches_tracked'))]
@@ -750,7 +846,13 @@ class Trainer:
                 global_batch = int(t.item())
         layers = (3, 4) if self.layer3_unfrozen else (4,)
         feats, saved = net.forward_train(img, keep_from=min(layers))
-        dfeat, lc = ce_loss(feats, targets, 1.0 / global_batch, want_grad=True)
+        if self.head_loss:
+            seed = self._seed_base + self.step_count + 1
+            logits = net.head_forward(feats, True, seed)
+            dlogits, lc = ce_loss(logits, targets, 1.0 / global_batch, want_grad=True)
+            dfeat = net.head_backward(feats, dlogits, seed)
+        else:
+            dfeat, lc = ce_loss(feats, targets, 1.0 / global_batch, want_grad=True)
         if self.world > 1:
             import torch.distributed as dist
             dist.all_reduce(lc, group=self.group)
@@ -795,7 +897,7 @@ class Trainer:
         a4, _ = self.net.range4
         st = {}
         if self.step_count:
-            for i, n in enumerate(self.l4_names):
+            for i, n in enumerate(self.opt_names):
                 lo, hi = self.net.offsets[n]
                 shp = self.net.params[n].shape
                 st[i] = {'step': torch.tensor(float(self.step_count)),
@@ -809,7 +911,7 @@ class Trainer:
         self.optimizer.load_state_dict(sd)
         a4, _ = self.net.range4
         steps = []
-        for i, n in enumerate(self.l4_names):
+        for i, n in enumerate(self.opt_names):
             s = sd['state'].get(i)
             if not s:
                 continue
@@ -831,4 +933,9 @@ class Trainer:
             net.nbt[k] = int(torch.as_tensor(sd[f'{k}.num_batches_tracked']).item())
         for k in head_keys():
             net.head_sd[k] = torch.as_tensor(sd[f'head.{k}']).clone()
+        if net.head_loss:
+            for i in (3, 7):
+                net.head_running[i][0].copy_(torch.as_tensor(sd[f'head.{i}.running_mean']))
+                net.head_running[i][1].copy_(torch.as_tensor(sd[f'head.{i}.running_var']))
+                net.head_nbt[i] = int(torch.as_tensor(sd[f'head.{i}.num_batches_tracked']).item())
         net.invalidate_packed()

@@ -35,7 +35,10 @@ Differences (documented in DESIGN.md / INTEGRATION.md):
   * extra flags: ``--precision {bf16,mixed,fp32}`` (default bf16 = throughput
     mode; mixed = the frozen stem/layers 1-3 in fp32 and layer4 in bf16, whose
     layer4 gradients track fp32 autograd to cosine >= 0.95),
-    ``--max-steps`` (stop an epoch early; benchmarking).
+    ``--max-steps`` (stop an epoch early; benchmarking), ``--head-loss``
+    (CrossEntropy and accuracy through model.head, trained with layer4: the
+    BinaryClassifier the merger and inference use; off by default, so C1 is
+    reproduced unless asked for).
   * TensorBoard is optional (not installed here): scalars are logged instead.
 """
 from __future__ import annotations
@@ -92,6 +95,10 @@ def parse_args(argv=None):
                         help='device compute precision (fp32 = the reference arithmetic; mixed = fp32 frozen prefix '
                              '+ bf16 layer4)')
     parser.add_argument('--max-steps', default=0, type=int, help='stop each epoch after this many steps (0 = all)')
+    parser.add_argument('--head-loss', action='store_true',
+                        help='train through model.head: CrossEntropy and accuracy on the BinaryClassifier head\'s two '
+                             'logits (train-mode BN + dropout), the head trained with layer4.  Default off: the '
+                             'reference computes them on the 512 pooled features and never calls the head (quirk C1)')
     return parser.parse_args(argv)
 
 
@@ -318,6 +325,8 @@ def _eval_pass(val_loader, model):
             continue
         maps, targets = model.maps(batch)
         feats = bb(maps)
+        if model.trainer.head_loss:  # --head-loss: the head in eval mode on the pooled features
+            feats = model.trainer.net.head_forward(feats, train=False)
         _, lc, pred = ce_loss(feats, targets, want_pred=True)
         ls, c = lc.tolist()
         loss_sum += ls
@@ -478,7 +487,7 @@ def main(argv=None):
     logging.info("Creating model with RANDOM weights...")
     base_sd, head_sd = st.init_state_dict(args.seed, args.model_name)
     trainer = st.Trainer(base_sd, head_sd, device, args.precision, lr=args.lr, group=group, world=world,
-                         model_name=args.model_name)
+                         model_name=args.model_name, head_loss=getattr(args, 'head_loss', False), seed=args.seed)
     frontend = st.TrainFrontEnd(device, args.precision)
     model = DeviceModel(trainer, frontend, rank, world, group)
 
