@@ -220,9 +220,10 @@ class Mode:
     backbone runs (two map slots; every step still takes its whole batch
     through every stage, the front end just starts one step early).  Round 5
     withdrew this after wrong logits in some pipelined steps; round 6 traced
-    them to the front end computing one power bin wrongly when it shared CUs
-    with the stem (a one-active-lane loop remainder, fixed in frontend.hip;
-    DESIGN.md 5c, tests/test_gpu_handoff.py), not to the hand-off.
+    them to the front end's packed-FP32 instructions returning wrong values
+    while MFMAs of the concurrent backbone ran on the same CUs, not to the
+    hand-off; libsad is built without those instructions (DESIGN.md 5c,
+    tests/test_gpu_handoff.py, tests/test_isa_scan.py).
 
     After the timed steps, ``run`` checks the LAST timed step's outputs: its
     merged logits must equal an untimed sequential forward of the same PCM bit

@@ -206,8 +206,19 @@ __device__ __forceinline__ void fe_standardise_segment(float* db, bool keep_db, 
   }
 }
 
-template <typename IT>  // int16_t PCM (scaled by 1/32768, torchaudio.load normalize) or float
-__global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
+// FM (frame-major, round 6, SAD_FE_FM=1, off by default): the dB map goes out
+// as [seg][frame][mel] -- each frame's 128 values are one 512-B row, so a lane
+// stores its mel rows straight from registers -- and fe_normalize_fm transposes
+// it while standardising.  Without the dB staging (16.9 KB) and the LDS twiddle
+// table (8 KB; read from global memory instead) a workgroup needs 46.6 KB of
+// LDS, so three fit on a CU and each SIMD holds three waves
+// (__launch_bounds__(256, 3): 168 VGPRs, 28 B of spills, no prefetch pipeline).
+// Measured slower: 2.89 vs 1.97 ms per 2,048 segments (same box, 3 rounds,
+// profiles/r06_ab_nopk.log) -- the third wave does not buy back the pipeline
+// and the re-read twiddles.  Bit-identical to the default form
+// (tests/test_gpu_frontend_fused.py).
+template <typename IT, bool FM = false>  // int16_t PCM (scaled by 1/32768, torchaudio.load normalize) or float
+__global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
     const IT* __restrict__ pcm, int64_t seg_stride, const int64_t* __restrict__ seg_offs, int64_t max_off,
     int n_samples,
     int n_frames, int hop,
@@ -216,13 +227,15 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     int n_mels, int bin_lo, int bin_hi, const int* __restrict__ lane_tab, const float* __restrict__ lane_w, int ml0,
     int ml1, float* __restrict__ out, int64_t n_seg, int xcd_map, int fuse, float top_db, float* __restrict__ map_out,
     unsigned* __restrict__ seg_cnt, float* __restrict__ seg_bmax) {
-  __shared__ float2 s_tw[FE_NC];
+  __shared__ float2 s_tw[FM ? 1 : FE_NC];
   __shared__ float2 s_buf[FE_WAVES][FE_ZBUF];
   __shared__ float2 s_tw3[64];  // W64^{q k2} at [k2][q]
   __shared__ float s_pow[FE_WAVES][FE_POW];
-  __shared__ float s_db[FE_STAGE_MELS][FE_FRAMES_PER_WG + 1];
+  __shared__ float s_db[FM ? 1 : FE_STAGE_MELS][FE_FRAMES_PER_WG + 1];
   __shared__ double s_red[16];
   __shared__ int s_last;
+  // the twiddle table: LDS (two-workgroup form) or global memory (FM)
+  auto twl = [&](int i) __attribute__((always_inline)) { return FM ? tw1024[i] : s_tw[i]; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // 1-D grid.  xcd_map: workgroup L -> segment 8 (L / 8 / n_fb) + L % 8, frame
@@ -246,8 +259,9 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
   const float in_scale = sizeof(IT) == 2 ? (1.0f / 32768.0f) : 1.0f;
   // staged: the mel rows by lane table (plan_create builds it when n_mels <=
   // FE_STAGE_MELS and the padded rows fit the power buffer), dB rows through LDS
-  const bool staged = lane_w != nullptr;
-  for (int i = tid; i < FE_NC; i += 256) s_tw[i] = tw1024[i];
+  const bool staged = FM || lane_w != nullptr;
+  if constexpr (!FM)
+    for (int i = tid; i < FE_NC; i += 256) s_tw[i] = tw1024[i];
   // this lane's mel rows (staged path) from the lane table: mm = the row (-1:
   // none), mk0 = its first bin - bin_lo; the power buffer's tail past bin_hi is
   // read (times a zero weight) by the padded rows: zero it once, the frames
@@ -266,10 +280,13 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
 
   // step 2's per-lane twiddles W1024^{l k1} (l = lane) in registers for all
   // frames; step 3's W64^{q k2} (q = lane & 3) as a [k2][q] LDS table
-  float2 tw2[16];
+  // (FM: re-read per frame from the global table instead, 30 registers fewer)
+  float2 tw2[FM ? 1 : 16];
+  if constexpr (!FM) {
 #pragma unroll
-  for (int k = 1; k < 16; ++k) tw2[k] = s_tw[(lane * k) & (FE_NC - 1)];
-  if (tid < 64) s_tw3[tid] = s_tw[(16 * (tid & 3) * (tid >> 2)) & (FE_NC - 1)];  // [k2][q]
+    for (int k = 1; k < 16; ++k) tw2[k] = twl((lane * k) & (FE_NC - 1));
+  }
+  if (tid < 64) s_tw3[tid] = twl((16 * (tid & 3) * (tid >> 2)) & (FE_NC - 1));  // [k2][q]
   __syncthreads();
   const int fg4 = lane >> 2, fq = lane & 3;
   const int fbr = (fq == 1 ? 2 : fq == 2 ? 1 : fq);  // bit-reversed q (output block of the lane)
@@ -290,7 +307,9 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
   // transformed (software pipeline: a frame's HBM latency no longer stalls its
   // wave).  The prefetch address is clamped into the segment, so it is always
   // valid; frames needing reflection (the first / last ones) take the slow path.
-  constexpr bool PREF = sizeof(IT) == 2;
+  // (FM: no software pipeline -- the third wave per SIMD hides the latency, and
+  // the 32 registers of the in-flight frame are what the occupancy needs)
+  constexpr bool PREF = sizeof(IT) == 2 && !FM;
   uint32_t pre[PREF ? 16 : 1];
   auto frame_inside = [&](int tt) { return pairs && tt * hop - pad >= 0 && tt * hop - pad + FE_NFFT <= n_samples; };
   auto prefetch = [&](int tt) __attribute__((always_inline)) {
@@ -308,6 +327,10 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
   if (PREF && pairs && n_samples >= FE_NFFT) prefetch(f_begin + wave);
 
   for (int t = f_begin + wave; t < f_end; t += FE_WAVES) {
+    // FM: an opaque zero per frame keeps the window and twiddle loads inside
+    // the loop (hoisted, they held 60 VGPRs across it and spilled)
+    int oz = 0;
+    if constexpr (FM) asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
     float2 x16[16];  // z[lane + 64 t'], t' = b + 4 r
     // ---- pass 0 input: z[m] = (y[2m], y[2m+1]) windowed, m = j + 256 r; one
     // 2-sample load per lane (coalesced) where the frame needs no reflection
@@ -315,7 +338,7 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     const bool inside = frame_inside(t);
     float2 wvs[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) wvs[q] = *(const float2*)(window + 2 * (lane + 64 * (q & 3) + 256 * (q >> 2)));
+    for (int q = 0; q < 16; ++q) wvs[q] = *(const float2*)(window + oz + 2 * (lane + 64 * (q & 3) + 256 * (q >> 2)));
     uint32_t cur[PREF ? 16 : 1];
     if constexpr (PREF) {
 #pragma unroll
@@ -331,7 +354,7 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
         float e0, e1;
         if (inside) {
           if constexpr (sizeof(IT) == 2) {
-            const uint32_t u = cur[b + 4 * r];
+            const uint32_t u = PREF ? cur[PREF ? b + 4 * r : 0] : *(const uint32_t*)(x + base + 2 * m);
             e0 = (float)(short)(u & 0xFFFF);
             e1 = (float)(short)(u >> 16);
           } else {
@@ -359,7 +382,8 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     // registers, twiddle, then a 4-point DFT across the lanes of a quad (DPP).
     dft16(x16);
 #pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) x16[fe_p16(k1)] = cmul(x16[fe_p16(k1)], tw2[k1]);
+    for (int k1 = 1; k1 < 16; ++k1)
+      x16[fe_p16(k1)] = cmul(x16[fe_p16(k1)], FM ? tw1024[oz + ((lane * k1) & (FE_NC - 1))] : tw2[FM ? 0 : k1]);
 #pragma unroll
     for (int k1 = 0; k1 < 16; ++k1) buf[k1 * 64 + (lane ^ (4 * k1))] = x16[fe_p16(k1)];
     wave_lds_sync();
@@ -386,13 +410,10 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     wave_lds_sync();
     // ---- real-spectrum recovery + power for bins [bin_lo, bin_hi]
     // Every lane runs the same trip count (the last round's surplus lanes
-    // compute a clamped bin and do not store it).  With `k <= bin_hi` as the
-    // loop bound, lane 63 had one bin fewer than the others (767 bins), and the
-    // compiler's pairwise-vectorised loop left that lane's last bin to a
-    // one-active-lane remainder loop; while the backbone's stem ran on another
-    // stream, that single-lane packed-FP32 sequence stored a power off by ~1e-3
-    // relative in about one frame in 10^6 (bin 705 = mel rows 124/125,
-    // tools/fe_concurrency.py).
+    // compute a clamped bin and do not store it), so no lane finishes the loop
+    // in a one-active-lane remainder.  (Round 6 first blamed that remainder for
+    // a wrong bin 705 beside the stem; the cause was the packed-FP32
+    // instructions, which the library no longer uses: csrc/Makefile NOPK)
     const int n_kit = (bin_hi - bin_lo + 64) / 64;
     for (int it = 0; it < n_kit; ++it) {
       const int k_raw = bin_lo + lane + 64 * it;
@@ -404,7 +425,7 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
       const float2 D = make_float2(A.x - B.x, A.y - B.y);
       const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);  // -i/2 (A - B)
       // e^{-2 pi i k / 2048}: the 1024-point table at k/2, times e^{-2 pi i / 2048} for odd k
-      float2 w2 = s_tw[(k >> 1) & (FE_NC - 1)];
+      float2 w2 = twl((k >> 1) & (FE_NC - 1));
       if (k == FE_NC) w2 = make_float2(-1.f, 0.f);
       if (k & 1) w2 = cmul(w2, make_float2(0.99999529380957619f, -0.0030679567629659761f));
       const float2 WO = cmul(w2, O);
@@ -427,8 +448,14 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
       for (int i = 0; i < ml0; ++i) a0 = fmaf(pa[i], wa[i * 64], a0);
 #pragma unroll 4
       for (int i = 0; i < ml1; ++i) a1 = fmaf(pb[i], wb[i * 64], a1);
-      if (mm[0] >= 0) s_db[mm[0]][t - f_begin] = 10.0f * log10f(fmaxf(a0, 1e-10f));
-      if (mm[1] >= 0) s_db[mm[1]][t - f_begin] = 10.0f * log10f(fmaxf(a1, 1e-10f));
+      if constexpr (FM) {  // frame-major: this frame's row of n_mels values
+        float* row = out + (seg * n_frames + t) * n_mels;
+        if (mm[0] >= 0) row[mm[0]] = 10.0f * log10f(fmaxf(a0, 1e-10f));
+        if (mm[1] >= 0) row[mm[1]] = 10.0f * log10f(fmaxf(a1, 1e-10f));
+      } else {
+        if (mm[0] >= 0) s_db[mm[0]][t - f_begin] = 10.0f * log10f(fmaxf(a0, 1e-10f));
+        if (mm[1] >= 0) s_db[mm[1]][t - f_begin] = 10.0f * log10f(fmaxf(a1, 1e-10f));
+      }
     } else {
       for (int m = lane; m < n_mels; m += 64) {
         const int k0 = mel_start[m], len = mel_len[m], off = mel_off[m];
@@ -439,7 +466,7 @@ __global__ __launch_bounds__(256, 2) void fe_mel_db_kernel(
     }
     wave_lds_sync();  // pw / buf are rewritten by the next frame
   }
-  if (staged) {
+  if (!FM && staged) {
     // [n_mels][frames of this block] -> rows of up to 32 consecutive frames
     __syncthreads();
     const int nf = f_end - f_begin;
@@ -589,6 +616,73 @@ __global__ __launch_bounds__(1024) void fe_normalize_kernel(float* db_io, int co
     const float v = fmaxf(x[i], floor_db);
     y[i] = (v - mean_f) / denom;
   }
+}
+
+// fe_normalize for the frame-major dB map of fe_mel_db<IT, true>: the same
+// statistics (max -> top-db clamp -> float64 mean / unbiased variance), then the
+// clamped dB map (db_out, optional) and the standardised map (map_out) written
+// mel-major [n_mels][n_frames] through a transpose in LDS (count floats of
+// dynamic LDS: one workgroup per CU, coalesced reads and writes).  In place:
+// every value is in registers before the first store (the reductions' barriers).
+__global__ __launch_bounds__(1024) void fe_normalize_fm_kernel(float* db_io, int n_mels, int n_frames, float top_db,
+                                                                float* db_out, float* map_out) {
+  extern __shared__ __attribute__((aligned(16))) float s_t[];
+  __shared__ double red[16];
+  __shared__ float redf[16];
+  const int count = n_mels * n_frames;
+  const int64_t seg = blockIdx.x;
+  const float* x = db_io + seg * count;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float v[kNormRegs];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < kNormRegs; ++k) {
+    const int i = tid + k * 1024;
+    v[k] = i < count ? x[i] : -INFINITY;
+    mx = fmaxf(mx, v[k]);
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if (lane == 0) redf[wave] = mx;
+  __syncthreads();
+  mx = redf[0];
+  for (int i = 1; i < 16; ++i) mx = fmaxf(mx, redf[i]);
+  const float floor_db = top_db >= 0.f ? mx - top_db : -INFINITY;
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < kNormRegs; ++k) {
+    if (tid + k * 1024 < count) {
+      v[k] = fmaxf(v[k], floor_db);
+      s += (double)v[k];
+    }
+  }
+  const double mean = block_sum_d(s, red) / count;
+  const float mean_f = (float)mean;
+  double ss = 0.0;
+#pragma unroll
+  for (int k = 0; k < kNormRegs; ++k)
+    if (tid + k * 1024 < count) {
+      const double d = (double)v[k] - mean;
+      ss += d * d;
+    }
+  const double var = block_sum_d(ss, red) / (count - 1);
+  const float denom = (float)sqrt(var + 0.0) + 1e-6f;
+  // frame-major i = frame * n_mels + mel -> mel-major mel * n_frames + frame
+  auto put = [&](float* dst, bool std) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < kNormRegs; ++k) {
+      const int i = tid + k * 1024;
+      if (i < count) {
+        const int f = i / n_mels, m = i - f * n_mels;
+        s_t[m * n_frames + f] = std ? (v[k] - mean_f) / denom : v[k];
+      }
+    }
+    __syncthreads();
+    float* o = dst + seg * count;
+    for (int i = tid; i < count; i += 1024) o[i] = s_t[i];
+    __syncthreads();
+  };
+  if (db_out) put(db_out, false);
+  put(map_out, true);
 }
 
 // Bilinear resize, align_corners=False (torchvision Resize on tensors; antialias
@@ -870,6 +964,16 @@ static int fe_xcd_map() {
   return v;
 }
 
+// SAD_FE_FM=1: the frame-major form (three workgroups per CU, measured slower;
+// see fe_mel_db_kernel) instead of the two-kernel staged form
+static int fe_fm() {
+  static const int v = [] {
+    const char* e = getenv("SAD_FE_FM");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <typename IT>
 static int frontend_run(const sad_frontend_plan* p, const IT* pcm, int64_t n_seg, int64_t seg_stride,
                         const int64_t* seg_offs, int64_t max_off, float* out_db, float* out_map,
@@ -885,20 +989,34 @@ static int frontend_run(const sad_frontend_plan* p, const IT* pcm, int64_t n_seg
   const int n_fb = (p->n_frames + FE_FRAMES_PER_WG - 1) / FE_FRAMES_PER_WG;
   const int count = p->cfg.n_mels * p->n_frames;
   const int fuse = p->d_seg_cnt != nullptr && count <= kNormRegs * 1024 ? fe_fused() : 0;
+  const size_t fm_lds = (size_t)count * sizeof(float);
+  const bool fm = !fuse && p->d_lane_w != nullptr && count <= kNormRegs * 1024 && fm_lds <= 150 * 1024 && fe_fm();
+  if (fm) {
+    static bool attr = [] {
+      return hipFuncSetAttribute((const void*)fe_normalize_fm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 150 * 1024) == hipSuccess;
+    }();
+    SAD_REQUIRE(attr, "fe_normalize_fm: dynamic LDS attribute");
+  }
   int64_t done = 0;
   while (done < n_seg) {
     const int64_t chunk = std::min<int64_t>(FE_CHUNK, n_seg - done);
     const size_t off = (size_t)done * count;
     const int xmap = fe_xcd_map();
     const unsigned blocks = (unsigned)((xmap ? (chunk + 7) / 8 * 8 : chunk) * n_fb);
-    hipLaunchKernelGGL(fe_mel_db_kernel<IT>, dim3(blocks), dim3(256), 0, s,
+    auto kfn = fm ? fe_mel_db_kernel<IT, true> : fe_mel_db_kernel<IT, false>;
+    hipLaunchKernelGGL(kfn, dim3(blocks), dim3(256), 0, s,
                        seg_offs ? pcm : pcm + done * seg_stride, seg_stride, seg_offs ? seg_offs + done : nullptr,
                        max_off, p->cfg.n_samples, p->n_frames, p->cfg.hop_length, p->d_tw1024, p->d_window,
                        p->d_mel_start, p->d_mel_len, p->d_mel_off, p->d_mel_w, p->nnz, p->cfg.n_mels, p->bin_lo,
                        p->bin_hi, p->d_lane_tab, p->d_lane_w, p->ml0, p->ml1, dbbuf + off, chunk, xmap, fuse, p->cfg.top_db,
                        out_map + off, p->d_seg_cnt, p->d_seg_bmax);
     SAD_CHECK_HIP(hipGetLastError());
-    if (!fuse) {
+    if (fm) {
+      hipLaunchKernelGGL(fe_normalize_fm_kernel, dim3((unsigned)chunk), dim3(1024), fm_lds, s, dbbuf + off,
+                         p->cfg.n_mels, p->n_frames, p->cfg.top_db, out_db ? out_db + off : nullptr, out_map + off);
+      SAD_CHECK_HIP(hipGetLastError());
+    } else if (!fuse) {
       hipLaunchKernelGGL(fe_normalize_kernel, dim3((unsigned)chunk), dim3(1024), 0, s, dbbuf + off, count,
                          p->cfg.top_db, out_map + off);
       SAD_CHECK_HIP(hipGetLastError());

@@ -1,7 +1,9 @@
 """GPU: the experimental one-kernel front end (SAD_FE_FUSED=1 fences / 2
 agent-scope stores: fe_mel_db's last workgroup per segment standardises the
 segment, csrc/frontend.hip) and the XCD-ordered grid (SAD_FE_XCD_MAP=1) against
-the default two-kernel form, bit for bit.  The settings are read once per
+the default two-kernel form, bit for bit; so is round 6's frame-major form
+(SAD_FE_FM=1: fe_mel_db<IT, true> + fe_normalize_fm, three workgroups per CU,
+the transpose in the normalisation; measured slower, off by default).  The settings are read once per
 process, so child processes compute the alternatives.  Cases: ragged batch
 sizes (the XCD-ordered grid is padded to a multiple of 8 segments), the
 clamped-dB output, the windows entry point, and a repeated launch (the fused
@@ -57,9 +59,10 @@ def _ours():
 
 
 @pytest.mark.parametrize('env', [{'SAD_FE_FUSED': '1'}, {'SAD_FE_FUSED': '2'},
-                                 {'SAD_FE_FUSED': '2', 'SAD_FE_XCD_MAP': '1'}, {'SAD_FE_XCD_MAP': '1'}])
+                                 {'SAD_FE_FUSED': '2', 'SAD_FE_XCD_MAP': '1'}, {'SAD_FE_XCD_MAP': '1'},
+                                 {'SAD_FE_FM': '1'}])
 def test_frontend_forms_equal_default(tmp_path, env):
-    for k in ('SAD_FE_FUSED', 'SAD_FE_XCD_MAP'):
+    for k in ('SAD_FE_FUSED', 'SAD_FE_XCD_MAP', 'SAD_FE_FM'):
         assert os.environ.get(k, '0') == '0', 'this test runs the default form in-process'
     path = str(tmp_path / 'alt.npz')
     code = CHILD.format(root=ROOT, pkg=os.path.join(ROOT, 'synthetic-audio-detection_amd'), sizes=SIZES, path=path)

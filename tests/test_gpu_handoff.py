@@ -4,14 +4,15 @@ Round 5 saw the pipelined bench (the next step's front end on a side stream
 during this step's backbone) produce wrong logits in some steps and took it for
 a cross-queue hand-off hole.  Round 6 located it (tools/handoff_study.py with
 HANDOFF_LOCATE=1, tools/fe_concurrency.py): the dispatch and barrier packets
-carry the right fence scopes, and the wrong values were in the MAPS -- one
-power bin (705: mel rows 124/125) of one frame, computed by the front end
-while the backbone's stem ran on another stream.  That bin was the only one
-the compiled recovery loop left to a one-active-lane remainder iteration;
-with a uniform trip count the failures are gone (0 of 160 against 10 of 40).
+carry the right fence scopes, and the wrong values were in the MAPS, computed
+by the front end while MFMAs of another kernel ran on the same CUs.  A kernel
+of bare MFMA chains does it too, a kernel of DPP / ds_bpermute / LDS traffic
+does not, and a front end built without packed-FP32 instructions
+(v_pk_fma/mul/add_f32) never does: libsad is built without them
+(csrc/Makefile NOPK; tests/test_isa_scan.py checks the library).
 
   * test_frontend_under_concurrent_stem: the case that failed, once, at a
-    batch where the old code failed almost surely (~25 % per 96 segments).
+    batch where the packed-FP32 build failed almost surely.
   * test_side_stream_handoffs: libsad consumers of tensors written on a torch
     side stream (as NCCL's stream hands back all-gathered logits or
     all-reduced gradients) after an event wait: the heads/merge, AdamW and the

@@ -12,6 +12,9 @@ REPS times each, and counts maps that differ bit for bit from a quiet run.
   lds       a kernel that only reads / writes its own 81,696 B of LDS (the
             stem's footprint), 256 threads: co-residency without the stem's code
   copy      large device-to-device copies (memory traffic, no LDS)
+  bperm / mfma / dpp / mix   probe_kernel: ONE feature of the stem (ds_bpermute,
+            MFMA chains, DPP + packed-int16 max, or all three) at the stem's LDS
+            footprint
 
 Build the probe kernels first (CPU side):
   hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/fence_diag.hip -o tools/_fence_diag.so"""
@@ -33,6 +36,8 @@ B = 96
 DUMP = os.environ.get('FE_DUMP', '')
 fl = ctypes.CDLL(os.path.join(ROOT, 'tools', '_fence_diag.so'))
 fl.lds_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+fl.probe_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+PROBES = {'bperm': 0, 'mfma': 1, 'dpp': 2, 'mix': 3}
 
 
 def main():
@@ -63,6 +68,8 @@ def main():
                 bb(bmaps)
             elif kind == 'lds':
                 assert fl.lds_launch(4096, 81696, 8, side.cuda_stream) == 0
+            elif kind in PROBES:  # one stem feature, the stem's LDS footprint (tools/fence_diag.hip probe_kernel)
+                assert fl.probe_launch(4096, 81696, PROBES[kind], 4000, side.cuda_stream) == 0
             elif kind == 'copy':
                 for _ in range(2):
                     big_b.copy_(big_a)
@@ -93,8 +100,13 @@ def main():
                             np.savez(os.path.join(DUMP, f'fe_fail_{kind}_{r}_{sg}_{fr}.npz'), seg=sg, frame=fr,
                                      got=db[sg, :, fr].cpu().numpy(), ref=ref_db[sg, :, fr].cpu().numpy(),
                                      pcm=pcm[sg].cpu().numpy())
-                    where.append(f'{int(d.sum())} values, segs {sorted(set(idx[:, 0].tolist()))[:4]}, rows '
-                                 f'{sorted(set(idx[:, 1].tolist()))[:6]}, frames {sorted(set(idx[:, 2].tolist()))[:4]}')
+                    segs = sorted(set(idx[:, 0].tolist()))
+                    s0 = segs[0]
+                    fr = sorted(set(idx[idx[:, 0] == s0][:, 2].tolist()))
+                    mel = sorted(set(idx[idx[:, 0] == s0][:, 1].tolist()))
+                    where.append(f'{int(d.sum())} values, {len(segs)} segs {segs[:4]}; seg {s0}: {len(mel)} mels '
+                                 f'{mel[:6]}, {len(fr)} frames {fr[:6]}, max |d| '
+                                 f'{(got[0] - exp[0]).abs().max().item():.3g}')
             print(f'{kind:9s} {form:8s}: {bad:2d} of {REPS} differ' + ('' if not where else '; e.g. ' + where[0]),
                   flush=True)
             for w in where[1:4]:
