@@ -55,11 +55,11 @@ DOMINANT = {
              'sad::halo256r_kernel (variant 31): patch-resident 256-channel x 16x16-pixel conv, weights streamed '
              'into registers; the stride-1 layer3/4 convs of a step (5 convs; layer3.0 conv2 + downsample runs as '
              'two image-range launches at micro-batch 2,048, the last one fuses the average pool)',
-             ('r05_pmc_traffic.json', 'r04_pmc_traffic.json')),
+             ('r06_pmc_traffic.json', 'r05_pmc_traffic.json')),
     'bf16x3': (30, 'sad::halo256_kernel<',
                'sad::halo256_kernel (variant 30), split-bf16: patch-resident 256-channel x 16x16-pixel conv; the '
                'stride-1 layer3/4 convs (the last one fuses the average pool)',
-               ('r05_pmc_traffic_bf16x3.json',)),
+               ('r06_pmc_traffic_bf16x3.json', 'r05_pmc_traffic_bf16x3.json')),
     'fp32': (13, 'sad::block_conv_kernel<float', 'sad::block_conv_kernel (variant 13), f32 MFMA', ()),
 }
 

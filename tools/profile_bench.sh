@@ -2,6 +2,9 @@
 # Kernel trace + HBM PMC passes of bench.py (GPU box, repo root):
 #   bash tools/profile_bench.sh TAG [extra bench args]
 # -> gpurun_out/prof_TAG/{trace,fetch,write}, summary gpurun_out/prof_TAG.md
+# (per-step figures over 10 backbone passes: 1 warm-up + 3 timed + the timed
+# output check's sequential forward + 5 isolated() passes of the overlapped run;
+# the side-stream front end adds one front end)
 set -e
 TAG=$1; shift
 ROOT=$GRAFT_REPO_ROOT
@@ -17,6 +20,6 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-forma
 T=$(find $OUT/trace -name 'run_kernel_trace.csv' | head -1 | xargs dirname)
 F=$(find $OUT/fetch -name 'run_counter_collection.csv' | head -1 | xargs dirname)
 W=$(find $OUT/write -name 'run_counter_collection.csv' | head -1 | xargs dirname)
-python3 tools/profsum.py --trace $T --fetch $F --write $W --steps 4 --json $OUT.traffic.json > $OUT.md
+python3 tools/profsum.py --trace $T --fetch $F --write $W --steps ${PROF_STEPS:-10} --json $OUT.traffic.json > $OUT.md
 tail -1 $OUT/trace.log >> $OUT.md
 cp $(find $OUT/trace -name 'run_kernel_stats.csv' | head -1) $OUT.stats.csv
