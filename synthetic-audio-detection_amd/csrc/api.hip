@@ -502,7 +502,7 @@ static int run_blocks(const sad_backbone_plan* p, size_t b0, size_t b1, int64_t 
 // activation is 64 MiB (bf16), so a conv's input, output and residual can stay
 // in the 256 MiB Infinity Cache; layers 2-4 run on the whole micro-batch (their
 // grids need the pixels, and bigger launches amortise the persistent kernels'
-// ramp and tail).  Same-box sweeps (tools/frontmb_ab.sh, "front:micro-batch"):
+// ramp and tail).  Same-box sweeps (round 2, "front:micro-batch"):
 // 32:512 46.9k seg/s vs 0:128 45.9k, 0:512 44.4-46.4k, 64:512 45.4k; 16 is 7%
 // slower (layer2's grids underfill).  At 32:128 one box measured -1.1%.
 // Round 2 at micro-batch 1024: 40 is 0.9 % and 48 1.4 % slower than 32 (same
