@@ -235,7 +235,9 @@ int sad_backbone_run_debug(const sad_backbone_plan* plan, const float* map, int6
  * planes, expansion 4, stride on conv2 as timm).  layers: blocks per stage
  * ([3,4,6,3] for resnet34/50).  params: 5 pointers per conv+BN in timm
  * state-dict order (conv1/bn1 first; per block its convs, then
- * downsample.0/downsample.1 where present). */
+ * downsample.0/downsample.1 where present).  dtype SAD_BF16X3 with
+ * SAD_BOTTLENECK runs every conv with the fourth split product W_lo.X_lo too
+ * (|dlogit| <= 1e-3 on resnet50; environment SAD_DEEP_X4=0: three products). */
 #define SAD_BASIC_BLOCK 0
 #define SAD_BOTTLENECK 1
 typedef struct sad_resnet_plan sad_resnet_plan;
@@ -317,7 +319,10 @@ int sad_conv2d_run(const void* in, int64_t N, int32_t H, int32_t W, int32_t Cin,
  * (oy*ss1, ox*ss1) of in1 [N,H1,W1,Cin1].  res (NULL or NHWC [N,Ho,Wo,Cout],
  * same dtype) is an identity shortcut added in the epilogue instead; it needs
  * the halo kernel (bf16, 3x3/s1/p1, H and W multiples of 16).
- * variant: 0 = default, 9..18 = implicit-GEMM tiles, 20 = halo (block.hip, halo.hip). */
+ * variant: 0 = default, 9..18 = implicit-GEMM tiles, 20 = halo (block.hip, halo.hip);
+ * | SAD_CONV_FOUR_PRODUCTS with dtype SAD_BF16X3: also W_lo.X_lo (the deep
+ * Bottleneck plans' form, on variants 9 / 13 / 15; 0 picks among them). */
+#define SAD_CONV_FOUR_PRODUCTS 0x10000
 int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t W, int32_t Cin, const void* in1,
                        int32_t H1, int32_t W1, int32_t Cin1, int32_t ss1, const void* wt, int32_t wt_ld,
                        const float* bias, const void* res, void* out, int32_t Cout, int32_t k,

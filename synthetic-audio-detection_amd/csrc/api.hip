@@ -977,6 +977,7 @@ extern "C" int sad_block_conv_run(const void* in0, int64_t N, int32_t H, int32_t
   a.Cout = Cout;
   a.relu = relu;
   a.M = N * a.Ho * a.Wo;
-  a.ablate = variant >> 8;  // timing-only ablation bits (tools/convbench.py --ablate)
+  a.ablate = (variant >> 8) & 255;  // timing-only ablation bits (tools/convbench.py --ablate)
+  a.x4 = (variant & SAD_CONV_FOUR_PRODUCTS) != 0;
   return launch_block_conv(a, dtype, (hipStream_t)stream, variant & 255);
 }

@@ -101,10 +101,15 @@ constexpr int block_smem_bytes_st() {
 // adds X_hi + X_lo exactly.
 // ST: training forward (bf16) -- the epilogue also sums the conv output and its
 // square per channel (StatAcc), one [2][BC] row per pixel-group workgroup wi.
-template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES, bool X3 = false, bool ST = false>
+// X4 (with X3): the fourth product W_lo.X_lo too -- the deep Bottleneck plans'
+// parity mode (resnet.hip: resnet50's 53 convs accumulate the dropped term past
+// 1e-3 on the logits, tools/deep_x3_budget.py), +33 % MFMA work.
+template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES, bool X3 = false, bool ST = false,
+          bool X4 = false>
 __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_kernel(BlockConvArgs a) {
   static_assert(S == 2 || S == 3, "ring depth");
   static_assert(!X3 || sizeof(T) == 2, "split-bf16 operands are bf16");
+  static_assert(!X4 || (X3 && !ST), "X4 is the split-bf16 inference form's fourth product");
   constexpr int NW = WC * WP;
   constexpr int BC = 16 * TC * WC, BP = 16 * TP * WP;  // channels x pixels per tile
   constexpr int ES = sizeof(T);
@@ -389,6 +394,12 @@ __global__ __launch_bounds__(64 * WC * WP, OCC * WC * WP / 4) void block_conv_ke
       for (int i = 0; i < TC; ++i)
 #pragma unroll
         for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], X3 ? pf[j] : pg[j], acc[i][j]);  // X3: W_lo . X_hi
+      if constexpr (X4) {  // W_lo . X_lo
+#pragma unroll
+        for (int i = 0; i < TC; ++i)
+#pragma unroll
+          for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[i], pg[j], acc[i][j]);
+      }
       SAD_STAMP(3);
     } else {
     if (do_issue) issue(ist);
@@ -425,6 +436,12 @@ if constexpr (X3) {
       for (int i = 0; i < TC; ++i)
 #pragma unroll
         for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[0][i], pf[1][j], acc[i][j]);
+      if constexpr (X4) {
+#pragma unroll
+        for (int i = 0; i < TC; ++i)
+#pragma unroll
+          for (int j = 0; j < TP; ++j) mfma_chunk<T>(wf[1][i], pf[1][j], acc[i][j]);
+      }
     } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -439,7 +456,7 @@ if constexpr (X3) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, (X3 ? 3 : 2) * TC * TP - (TC + TP), 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, (X4 ? 4 : X3 ? 3 : 2) * TC * TP - (TC + TP), 0);
     }
     st = st + 1 == S ? 0 : st + 1;
     if (++cks == nk) {
@@ -607,7 +624,7 @@ if constexpr (X3) {
 }
 
 template <typename T, int WC, int WP, int TC, int TP, int S, int OCC, bool RES_OK = false, bool X3 = false,
-          bool ST_OK = false>
+          bool ST_OK = false, bool X4 = false>
 static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
   constexpr int smem0 = block_smem_bytes<WC, WP, TC, TP, S, OCC>();
   static_assert(smem0 * OCC <= 160 * 1024, "LDS budget");
@@ -615,9 +632,10 @@ static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
   const int smem = a.st_part ? block_smem_bytes_st<WC, WP, TC, TP, S, OCC>() : smem0;
   SAD_REQUIRE(RES_OK || !a.res, "this block-conv variant has no epilogue residual (variants 13, 20, 21, 25 do)");
   SAD_REQUIRE(16 * TP * WP / 8 / (WC * WP) <= 4 || a.KH * a.KW <= 32, "variants 16 / 19: at most 32 filter taps");
-  const void* kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3>;
+  static_assert(!(ST_OK && X4), "no fused statistics in the four-product form");
+  const void* kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3, false, X4>;
   if constexpr (RES_OK) {
-    if (a.res) kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true, X3>;
+    if (a.res) kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true, X3, false, X4>;
   }
   if constexpr (ST_OK) {
     if (a.st_part) kfn = (const void*)block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3, true>;
@@ -656,13 +674,14 @@ static int launch_block_t(const BlockConvArgs& a, hipStream_t s) {
   }
   if constexpr (RES_OK) {
     if (a.res) {
-      hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true, X3>), dim3((unsigned)g),
+      hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, true, X3, false, X4>), dim3((unsigned)g),
                          dim3(64 * WC * WP), smem, s, a);
       SAD_CHECK_HIP(hipGetLastError());
       return SAD_OK;
     }
   }
-  hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3>), dim3((unsigned)g), dim3(64 * WC * WP),
+  hipLaunchKernelGGL((block_conv_kernel<T, WC, WP, TC, TP, S, OCC, false, X3, false, X4>), dim3((unsigned)g),
+                     dim3(64 * WC * WP),
                      smem, s, a);
   SAD_CHECK_HIP(hipGetLastError());
   return SAD_OK;
@@ -692,6 +711,17 @@ static int launch_block_v(const BlockConvArgs& a, int v, hipStream_t s) {
     case 19: return launch_block_t<T, 1, 8, 8, 4, 2, 1, false, X3>(a, s);
   }
   set_error("unknown block-conv variant");
+  return SAD_ERR_ARG;
+}
+// the four-product split-bf16 form (BlockConvArgs.x4): the implicit-GEMM
+// variants gemm_block_variant picks (Cout 64, 128, multiples of 256)
+static int launch_block_x4(const BlockConvArgs& a, int v, hipStream_t s) {
+  switch (v) {
+    case 9: return launch_block_t<u16, 1, 4, 4, 4, 2, 2, false, true, false, true>(a, s);
+    case 13: return launch_block_t<u16, 2, 4, 8, 4, 2, 1, true, true, false, true>(a, s);
+    case 15: return launch_block_t<u16, 2, 4, 4, 4, 3, 1, false, true, false, true>(a, s);
+  }
+  set_error("four-product split-bf16 convs run on the implicit-GEMM variants 9, 13, 15");
   return SAD_ERR_ARG;
 }
 
@@ -1130,8 +1160,11 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   SAD_REQUIRE(a.Cout % 64 == 0 && a.out_pstride % 4 == 0, "Cout / output stride");
   SAD_REQUIRE(a.in0_pstride % (16 / ES) == 0 && (!a.in1 || a.in1_pstride % (16 / ES) == 0), "input strides");
   if (a.M == 0) return SAD_OK;
-  const int v = variant > 0 ? variant : default_block_variant(a_in, dtype);
+  // x4 (the deep Bottleneck plans' parity mode): every conv on the implicit GEMM
+  const int v = variant > 0 ? variant : a.x4 ? gemm_block_variant(a_in) : default_block_variant(a_in, dtype);
   SAD_REQUIRE(variant_fits(v, a.Cout), "variant's channel tile does not divide Cout");
+  SAD_REQUIRE(!a.x4 || (dtype == SAD_BF16X3 && !a.st_part && !a.pool_out && (v == 9 || v == 13 || v == 15)),
+              "four-product convs: split-bf16 inference on variants 9 / 13 / 15, no fused statistics or pool");
   ++g_block_conv_kernels;
   if (v == 30) {
     SAD_REQUIRE(dtype != SAD_F32 && halo256_ok(a_in), "variant 30: bf16 / split-bf16 3x3/s1/p1, Cout % 256, 16 x 16 tiles");
@@ -1210,7 +1243,9 @@ int launch_block_conv(const BlockConvArgs& a_in, int dtype, hipStream_t s, int v
   }
 #endif
   int rc;
-  if (dtype == SAD_BF16X3) {
+  if (dtype == SAD_BF16X3 && a.x4) {
+    rc = launch_block_x4(a, v, s);
+  } else if (dtype == SAD_BF16X3) {
     SAD_REQUIRE(v >= 9 && v <= 19, "split-bf16 runs on the implicit-GEMM variants 9..19");
     rc = launch_block_v<u16, true>(a, v, s);
   } else {

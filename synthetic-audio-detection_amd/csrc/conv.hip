@@ -489,7 +489,8 @@ __device__ __forceinline__ float dppf(float v) {
 // X3 (split-bf16 parity mode, SAD_BF16X3): the band is kept as hi and lo bf16
 // planes, the weights as hi and lo, each product is W_hi.X_hi + W_lo.X_hi +
 // W_hi.X_lo, and the pooled output is stored split ([hi 32 | lo 32] per 32
-// channels; one workgroup per CU for the larger LDS footprint).
+// channels; one workgroup per CU for the larger LDS footprint).  X4 adds
+// W_lo.X_lo (the deep Bottleneck plans, resnet.hip).
 constexpr int STEM_OPITCH_X3 = 288;  // 128 bf16 (64 ch hi + lo) + pad: 72 dwords -> 4 rows on disjoint bank sets
 // s_u holds, while the band is built, the x-interpolated rows + a zero row +
 // the [NBR] row table; afterwards the pooled-row staging + the wave-edge exchange
@@ -511,9 +512,10 @@ constexpr int stem_u_floats() {
 // owns (2*py0 .. 2*py0 + 2P - 1; the carry-in row belongs to the previous one)
 // feeds per-channel sums of y and y^2 -> a.part[workgroup][2][64] (the
 // bn_reduce_kernel partial format) for the batch statistics.
-template <bool X3, bool TRAIN = false>
+template <bool X3, bool TRAIN = false, bool X4 = false>
 __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) {
   static_assert(!(X3 && TRAIN), "the training stem is bf16");
+  static_assert(!X4 || X3, "X4: the split stem's fourth product");
   constexpr int OPITCH = X3 ? STEM_OPITCH_X3 : STEM_OPITCH;
   __shared__ __attribute__((aligned(16))) u16 s_img[STEM_BAND_ROWS * STEM_BPITCH];
   __shared__ __attribute__((aligned(16))) u16 s_imgl[X3 ? STEM_BAND_ROWS * STEM_BPITCH : 8];
@@ -729,6 +731,10 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
           for (int j = 0; j < 4; ++j) mfma_chunk<u16>(av, bwl[j][s], r[i][j]);  // X_hi . W_lo
 #pragma unroll
           for (int j = 0; j < 4; ++j) mfma_chunk<u16>(al, bw[j][s], r[i][j]);   // X_lo . W_hi
+          if constexpr (X4) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mfma_chunk<u16>(al, bwl[j][s], r[i][j]);  // X_lo . W_lo
+          }
         }
       }
     }
@@ -1052,6 +1058,8 @@ int launch_stem(const StemArgs& a, int dtype, hipStream_t s) {
   }
   if (dtype == SAD_BF16)
     hipLaunchKernelGGL(stem_bf16_kernel<false>, dim3(128 / STEM_P, (unsigned)a.B), dim3(256), 0, s, a);
+  else if (dtype == SAD_BF16X3 && a.x4)
+    hipLaunchKernelGGL((stem_bf16_kernel<true, false, true>), dim3(128 / STEM_P, (unsigned)a.B), dim3(256), 0, s, a);
   else if (dtype == SAD_BF16X3)
     hipLaunchKernelGGL(stem_bf16_kernel<true>, dim3(128 / STEM_P, (unsigned)a.B), dim3(256), 0, s, a);
   else

@@ -76,6 +76,8 @@ struct BlockConvArgs {
   float* st_part;        // training (bf16): fused BN statistics, fp32 [rows][2][Cout] sums of the
                          // conv output and its square per workgroup row (variants 13, 15, 20, 25)
   int* st_rows;          // host out: rows written to st_part by the launch
+  int x4;                // split-bf16: also the fourth product W_lo.X_lo (the deep Bottleneck plans,
+                         // resnet.hip); runs on the implicit-GEMM variants
 };
 
 // Fused layer1 BasicBlock (l1block.hip, variant 40): bf16 NHWC, 64 channels,
@@ -113,6 +115,7 @@ struct StemArgs {
   const float* w3;       // [64][3][49] fp32 conv1 with bn1's scale folded (the stem3 kernel's weights)
   const u16* img16;      // training stem: [B, 512, 512] bf16 image (bias = bn1 gamma, w unfolded)
   float* part;           // training stem: per-workgroup [2][64] sums of y, y^2
+  int x4;                // split-bf16: also the fourth product W_lo.X_lo (resnet.hip's Bottleneck plans)
 };
 
 int launch_conv(const ConvArgs& a, int dtype, hipStream_t s, int variant = 0);

@@ -24,6 +24,7 @@
 // default_block_variant: the resident-weight / halo kernels for the 3x3/s1
 // convs that qualify); BN is folded into weights and bias.
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <vector>
@@ -81,6 +82,14 @@ int fold_conv(const float* const* q, int cout, int cin, int k, int dtype, ConvW&
   return upload((void**)&out.b, b);
 }
 
+bool deep_x4() {
+  static const bool on = [] {
+    const char* e = getenv("SAD_DEEP_X4");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 void free_conv(ConvW& c) {
   (void)hipFree(c.w);
   (void)hipFree(c.b);
@@ -92,6 +101,11 @@ void free_conv(ConvW& c) {
 
 struct sad_resnet_plan {
   int dtype, mh, mw, block, num_features;
+  // split-bf16 Bottleneck plans: the fourth product W_lo.X_lo in every conv
+  // (all on the implicit GEMM) -- resnet50's 53 convs otherwise accumulate the
+  // dropped term to ~1.05e-3 on the logits (tools/deep_x3_budget.py: 6.8e-4
+  // with it).  SAD_DEEP_X4=0 keeps the three-product form.
+  int x4 = 0;
   void* stem_w = nullptr;
   float* stem_b = nullptr;
   float* stem_w3 = nullptr;  // distinct-channel stem (sad_resnet_run_img3)
@@ -140,6 +154,7 @@ extern "C" int sad_resnet_plan_create(const float* const* params, int32_t n_para
   p->mw = map_w;
   p->block = block;
   p->num_features = 512 * exp;
+  p->x4 = dtype == SAD_BF16X3 && block == SAD_BOTTLENECK && deep_x4();
   int rc;
   if ((rc = fold_stem(params, dtype, &p->stem_w, &p->stem_b, &p->stem_w3))) {
     sad_resnet_plan_destroy(p);
@@ -239,6 +254,7 @@ static int rn_block_conv(const sad_resnet_plan* p, const ConvW& c, const void* x
   a.Cout = c.cout;
   a.relu = 1;
   a.M = n * Ho * Ho;
+  a.x4 = p->x4;
   return launch_block_conv(a, p->dtype, s);
 }
 
@@ -246,8 +262,9 @@ static int rn_block_conv(const sad_resnet_plan* p, const ConvW& c, const void* x
 // (ResNet-18's plan, api.hip run_blocks): stride 1, no downsample, 16 x 16
 // tiles, Cout <= 64, or Cout <= 128 where layer2 runs the halo / resident-weight
 // kernels (the split-bf16 mode's variant 31 takes the identity as K columns)
-static bool identity_epilogue(int dtype, const Block& b, int Ho) {
-  if (!(dtype == SAD_BF16 || dtype == SAD_BF16X3) || b.stride != 1 || b.has_ds || Ho % 16 != 0) return false;
+static bool identity_epilogue(const sad_resnet_plan* p, const Block& b, int Ho) {
+  const int dtype = p->dtype;
+  if (p->x4 || !(dtype == SAD_BF16 || dtype == SAD_BF16X3) || b.stride != 1 || b.has_ds || Ho % 16 != 0) return false;
   return b.cout <= 64 || (b.cout <= 128 && layer2_halo() && !(dtype == SAD_BF16 && layer2_v31()) &&
                           !(dtype == SAD_BF16X3 && x3_layer2_v31()));
 }
@@ -261,6 +278,7 @@ static int rn_chunk(const sad_resnet_plan* p, const float* map, const float* img
   void* T2 = ws + 3 * ab;
   int rc;
   StemArgs st{map, img, p->mh, p->mw, p->stem_w, p->stem_b, X, n, img3, p->stem_w3};
+  st.x4 = p->x4;
   if ((rc = launch_stem(st, p->dtype, s))) return rc;
   int H = 128, C = 64;
   for (const Block& b : p->blocks) {
@@ -283,7 +301,7 @@ static int rn_chunk(const sad_resnet_plan* p, const float* map, const float* img
         if ((rc = launch_l1block(f, s))) return rc;
       } else {
         if ((rc = rn_block_conv(p, b.c1, X, n, H, b.stride, nullptr, 0, 0, 1, T1, s))) return rc;
-        if (identity_epilogue(p->dtype, b, Ho)) {
+        if (identity_epilogue(p, b, Ho)) {
           // identity blocks of layer1/2: the shortcut as an epilogue add on the
           // halo / resident-weight kernels (as ResNet-18's plan), not as identity
           // K columns on the implicit GEMM

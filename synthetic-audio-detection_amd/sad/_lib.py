@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get('SAD_LIB', os.path.join(_HERE, 'libsad.so'))
 SAD_F32 = 0
 SAD_BF16 = 1
 SAD_BF16X3 = 2  # split-bf16 parity mode (include/sad.h)
+SAD_CONV_FOUR_PRODUCTS = 0x10000  # sad_block_conv_run variant flag (include/sad.h)
 DTYPES = {'fp32': SAD_F32, 'bf16': SAD_BF16, 'bf16x3': SAD_BF16X3}
 SAD_PCM_I16 = 0  # sad_pcm_format
 SAD_PCM_F32 = 1

@@ -477,9 +477,10 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int = 1
 def block_conv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int = 1, pad: int = 1,
                sc: torch.Tensor | None = None, sc_stride: int = 1, relu: bool = True, variant: int = 0,
                out: torch.Tensor | None = None, res: torch.Tensor | None = None, k: int = 3,
-               split: bool = False) -> torch.Tensor:
+               split: bool = False, four: bool = False) -> torch.Tensor:
     """conv(x) + 1x1 shortcut(sc) [+ res] as ONE launch (libsad block-conv kernels).
-    split=True: every tensor in the split-bf16 layout (``to_split``; dtype 'bf16x3').
+    split=True: every tensor in the split-bf16 layout (``to_split``; dtype 'bf16x3');
+    four=True (with split): the four-product form of the deep Bottleneck plans.
     x [N,H,W,Cin], sc [N,H1,W1,Cin1] or None, w [Cout, wt_ld] with the k*k*Cin
     conv taps first and the shortcut's Cin1 columns next (extra columns are
     ignored), bias [Cout] fp32, res [N,Ho,Wo,Cout] (epilogue identity shortcut)."""
@@ -500,5 +501,6 @@ def block_conv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int
     with torch.cuda.device(x.device):
         _lib.call('sad_block_conv_run', _lib.ptr(x), N, H, W, Cin, _lib.ptr(sc), H1, W1, Cin1, sc_stride,
                   _lib.ptr(w), wt_ld, _lib.ptr(bias), _lib.ptr(res), _lib.ptr(out), Cout, k, stride, pad,
-                  int(relu), dt, variant, _lib.stream_handle(x.device))
+                  int(relu), dt, variant | (_lib.SAD_CONV_FOUR_PRODUCTS if four else 0),
+                  _lib.stream_handle(x.device))
     return out

@@ -6,10 +6,11 @@ its waveform_to_spectrogram glue).  The models: 2 heads on one shared backbone
 (sad.weights seed 0) with the committed calibrated BN statistics.
 
 Tolerance: |dlogit| <= 1e-3 (north star) for fp32 and for the split-bf16
-parity mode (bf16x3) on resnet34, and identical decisions.  resnet50's 16
-Bottlenecks carry more summation-order noise: its fp32 path is 2.4e-4 from the
-fixture, bf16x3 1.05e-3 (measured), so bf16x3 on resnet50 gets 2e-3 (decisions
-still identical).  bf16 is reported with the bar of the bf16 noise it carries
+parity mode (bf16x3), and identical decisions.  resnet50's 53 convs carry
+more summation-order noise (fp32: 2.4e-4 from the fixture); in bf16x3 they
+accumulated the dropped W_lo.X_lo term to 1.05e-3, so the Bottleneck plans run
+the four-product form (csrc/resnet.hip x4; tools/deep_x3_budget.py emulates
+6.8e-4 with it).  bf16 is reported with the bar of the bf16 noise it carries
 (resnet50's pooled features are ~7e-2 off in bf16): 0.25 for
 resnet34, 0.5 for resnet50 (measured 0.245 merged / 0.398 per head with the
 layer3/4 3x3 convs on variant 31, 0.26 / <= 0.25 on variant 13: the two sum K
@@ -44,7 +45,7 @@ def _sd(name):
 def test_deep_logits_match_reference(golden_frontend, name, dtype):
     from oracle.decision import interpret_multihead_logits
     from sad.engine import Engine
-    tol = {'fp32': 1e-3, 'bf16x3': 2e-3 if name == 'resnet50' else 1e-3, 'bf16': 0.5 if name == 'resnet50' else 0.25}[dtype]
+    tol = {'fp32': 1e-3, 'bf16x3': 1e-3, 'bf16': 0.5 if name == 'resnet50' else 0.25}[dtype]
     fx = dict(np.load(os.path.join(GOLDEN, 'golden_deep.npz')))
     pcm = torch.from_numpy(golden_frontend['pcm']).to(DEV)
     eng = Engine(_sd(name), DEV, dtype=dtype, micro_batch=3)  # 4 = 3 + 1: a micro-batch boundary

@@ -4,8 +4,8 @@ CPU oracle, end to end from the golden maps to the merged logits.
 
 The hash-seeded weights get BN running statistics calibrated on the test maps
 themselves (oracle in train mode, cumulative averages), so activations stay
-O(1) through 16-33 blocks.  Tolerances: fp32 mode |dlogit| <= 1e-3 (the
-north-star bar); bf16 mode pooled features relative error <= 5e-2 / 1e-1 / 2e-1
+O(1) through 16-33 blocks.  Tolerances: fp32 and split-bf16 (bf16x3) modes
+|dlogit| <= 1e-3 (the north-star bar); bf16 mode pooled features relative error <= 5e-2 / 1e-1 / 2e-1
 for resnet34 / 50 / 101 (reported, not the parity gate).  parity pinned only through the oracle (no reference
 fixture exists for these backbones)."""
 import numpy as np
@@ -59,6 +59,14 @@ def test_deep_resnet_vs_oracle(name, maps):
     print(f'{name} fp32: pooled rel err {df:.3e}, max|dlogit| {d:.3e}')
     assert np.isfinite(merged.cpu().numpy()).all()
     assert d <= 1e-3
+
+    # the split-bf16 parity mode: four products in the Bottleneck plans
+    eng3 = Engine(sd, DEV, dtype='bf16x3', micro_batch=2)
+    _, merged3 = eng3.forward_maps(maps.to(DEV))
+    torch.cuda.synchronize()
+    d3 = (merged3.cpu() - ref).abs().max().item()
+    print(f'{name} bf16x3: max|dlogit| {d3:.3e}')
+    assert d3 <= 1e-3
 
     eng16 = Engine(sd, DEV, dtype='bf16', micro_batch=3)
     f16 = eng16.backbones[0](maps.to(DEV))

@@ -97,6 +97,73 @@ def test_block_conv_x3_vs_float64(cin, cout, H, stride, shortcut, variant):
     assert err <= 1e-4, err
 
 
+def _parts(t):
+    hi = t.to(torch.bfloat16).float()
+    return hi, (t - hi).to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize('cin,cout,H,k,stride,shortcut,variant', [
+    (64, 64, 32, 1, 1, None, 9),          # a Bottleneck conv1 (1x1, width 64)
+    (64, 64, 32, 3, 1, None, 9),          # its 3x3 conv2
+    (128, 128, 32, 3, 2, None, 15),       # layer2.0 conv2 (3x3/s2, width 128)
+    (128, 256, 16, 1, 1, 'res', 13),      # conv3 + identity as the epilogue residual
+    (64, 256, 32, 1, 1, 'downsample', 13),  # conv3 + the 1x1 downsample as K columns
+    (256, 512, 16, 1, 1, None, 15),       # small grid: variant 15
+])
+def test_block_conv_four_products(cin, cout, H, k, stride, shortcut, variant):
+    """The four-product split-bf16 form (SAD_CONV_FOUR_PRODUCTS: + W_lo.X_lo,
+    the deep Bottleneck plans' convs, resnet.hip) against float64 convs of the
+    same split operands, next to the three-product form on the same variant:
+    each is closer (RMS over the output) to its own arithmetic's reference than
+    to the other's, and the four-product result is within 1e-4 of the output
+    scale of the exact conv of the stored operands."""
+    from sad.engine import block_conv, from_split, to_split
+    g = torch.Generator().manual_seed(cin + 3 * cout + H + k)
+    N = 3
+    x = torch.randn(N, H, H, cin, generator=g).clamp_min(0)
+    w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (k * k * cin)) ** 0.5
+    bias = torch.randn(cout, generator=g) * 0.1
+    Ho = (H + 2 * (k // 2) - k) // stride + 1
+    wk = w.permute(0, 2, 3, 1).reshape(cout, k * k * cin)
+    sc = wsc = res = None
+    if shortcut == 'downsample':
+        sc = torch.randn(N, 2 * Ho, 2 * Ho, 2 * cin, generator=g).clamp_min(0)
+        wsc = torch.randn(cout, 2 * cin, generator=g) * (1.0 / (2 * cin)) ** 0.5
+    elif shortcut == 'res':
+        res = torch.randn(N, Ho, Ho, cout, generator=g).clamp_min(0)
+    wfull = torch.cat([wk, wsc], 1) if sc is not None else wk
+    xs, ws = from_split(to_split(x)), from_split(to_split(wfull))  # the stored operand values
+    scs = from_split(to_split(sc)) if sc is not None else None
+    rs = from_split(to_split(res)).double() if res is not None else 0
+    w4 = ws[:, :k * k * cin].reshape(cout, k, k, cin).permute(0, 3, 1, 2)
+    wsc4 = ws[:, k * k * cin:] if sc is not None else None
+
+    def pre(xv, wv, scv, wscv):  # conv [+ shortcut] in float64, no bias / ReLU
+        return _conv_ref(xv, wv, stride, k // 2, scv, wscv, 2, None, relu=False)
+
+    full = pre(xs, w4, scs, wsc4)
+    xl, wl = _parts(xs)[1], _parts(w4)[1]
+    lolo = pre(xl, wl, _parts(scs)[1] if sc is not None else None, _parts(wsc4)[1] if sc is not None else None)
+    post = lambda y: (y + bias.double().view(1, 1, 1, -1) + rs).clamp_min(0)  # noqa: E731
+    ref4, ref3 = post(full), post(full - lolo)
+    outs = {}
+    for four in (False, True):
+        out = block_conv(to_split(x).to(DEV), to_split(wfull).to(DEV), bias.to(DEV), stride=stride, pad=k // 2,
+                         sc=to_split(sc).to(DEV) if sc is not None else None, sc_stride=2,
+                         res=to_split(res).to(DEV) if res is not None else None, variant=variant, k=k,
+                         split=True, four=four)
+        torch.cuda.synchronize()
+        outs[four] = from_split(out.cpu()).double()
+    rms = lambda a, b: ((a - b) ** 2).mean().sqrt().item()  # noqa: E731
+    d4, d4x = rms(outs[True], ref4), rms(outs[True], ref3)
+    d3, d3x = rms(outs[False], ref3), rms(outs[False], ref4)
+    err = ((outs[True] - ref4).abs().max() / ref4.abs().max()).item()
+    print(f'four products {cin}->{cout} k{k} s{stride} {shortcut} v{variant}: rms vs 4-ref {d4:.3e} '
+          f'(vs 3-ref {d4x:.3e}); three products rms vs 3-ref {d3:.3e} (vs 4-ref {d3x:.3e}); max rel {err:.3e}')
+    assert d4 < d4x and d3 < d3x
+    assert err <= 1e-4, err
+
+
 @pytest.mark.parametrize('c,H,res,variant', [(64, 32, True, 20), (64, 48, False, 20), (128, 16, True, 20),
                                              (128, 32, False, 20), (64, 32, True, 26), (64, 48, False, 26),
                                              (64, 16, True, 26), (64, 80, True, 26),

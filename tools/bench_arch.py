@@ -52,6 +52,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--heads', type=int, default=6)
     ap.add_argument('--micro-batch', type=int, default=64)
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'bf16x3', 'fp32'])
     args = ap.parse_args()
     from sad import _lib
     from sad import weights as sw
@@ -62,7 +63,8 @@ def main():
     pcm = torch.empty(B, SEG, dtype=torch.int16, device=dev)
     _lib.call('sad_synth_pcm', 0, 0, B, SEG, _lib.ptr(pcm), _lib.stream_handle(dev))
     for name in args.arch:
-        eng = Engine(sw.merged_state_dict(0, args.heads, False, model_name=name), dev, 'bf16', args.micro_batch)
+        eng = Engine(sw.merged_state_dict(0, args.heads, False, model_name=name), dev, args.dtype,
+                     args.micro_batch)
         ev = []
 
         def step(timed):
@@ -88,7 +90,7 @@ def main():
         fl = backbone_flop(name)
         tf = fl * B / (bb_ms * 1e-3) / 1e12
         print(json.dumps({'arch': name, 'segments_per_s': round(B * args.steps / el, 1), 'batch': B,
-                          'heads': args.heads, 'micro_batch': eng.backbones[0].micro_batch, 'dtype': 'bf16',
+                          'heads': args.heads, 'micro_batch': eng.backbones[0].micro_batch, 'dtype': args.dtype,
                           'backbone_ms_per_step': round(bb_ms, 3), 'backbone_gflop_per_segment': round(fl / 1e9, 3),
                           'backbone_tflops': round(tf, 1), 'frac_of_bf16_peak': round(tf / BF16_PEAK_TFLOPS, 4),
                           'finite': bool(torch.isfinite(merged).all().item())}), flush=True)
