@@ -678,23 +678,13 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
   const int fr = lane & 15, fg = lane >> 4;
 
   // raw conv row cr for this wave's 64 conv columns: r[i][j] = C[ch j*16+fg*4+e][px 64w+16i+fr]
+  // (cr >= 0: only the first workgroup's carry-in row, conv row -1, lies above
+  // the image; the caller fills it with -inf, which never wins the max)
   auto conv_row = [&](int cr, f32x4 (&r)[4][4]) __attribute__((always_inline)) {
-    if (cr < 0) {  // above the image: never wins the max
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) r[i][j] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-      return;
-    }
-    // the plain bf16 stem starts the accumulators at the bias: max-pooling
-    // relu(x + b) is relu(max(x + b)), and the epilogue then adds nothing
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float b0 = (!X3 && !TRAIN) ? s_bias[j * 16 + fr] : 0.f;
-        r[i][j] = f32x4{b0, b0, b0, b0};
-      }
+    // accumulators start at zero (the MFMA's inline-constant C operand: no
+    // register copies); the bias goes in after the max-pool (relu(max(x) + b)
+    // == max(relu(x + b)))
+    const f32x4 init[4] = {};
     const int rb = 2 * (cr - 2 * py0) + 2;
     uint4 bw[4][2];  // weight fragments (LDS-resident; re-read per row keeps VGPRs for the pool)
     uint4 bwl[X3 ? 4 : 1][2];
@@ -718,7 +708,10 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
         av.z = *(const uint32_t*)(p + 4);
         av.w = *(const uint32_t*)(p + 6);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mfma_chunk<u16>(av, bw[j][s], r[i][j]);  // C[px][ch]
+        for (int j = 0; j < 4; ++j)  // C[px][ch]
+          r[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av),
+                                                            __builtin_bit_cast(bf16x8, bw[j][s]),
+                                                            s == 0 ? init[j] : r[i][j], 0, 0, 0);
         if constexpr (X3) {
           const u16* pl = s_imgl + o;
           uint4 al;
@@ -753,27 +746,50 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
           st_q[j] += r[i][j][e] * r[i][j][e];
         }
   };
-  f32x4 carry[4][4], cur[4][4];
-  conv_row(2 * py0 - 1, carry);
-  for (int pi = 0; pi < STEM_P; ++pi) {
+  // conv row 2py+1 is the next pooled row's first: two carry sets alternate
+  // (pooled rows in pairs), so the carried row needs no register copies
+  f32x4 ca[4][4], cb[4][4], cur[4][4];
+  if (py0 == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ca[i][j] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  } else {
+    conv_row(2 * py0 - 1, ca);
+  }
+  // the vertical max as one v_med3_f32 (x, y, +inf) = max(x, y): fmaxf would
+  // first canonicalise each MFMA result (two more VALU per value), and an
+  // inline-asm v_max would escape the compiler's MFMA result-hazard waits; no
+  // NaN reaches it.  (The training stem keeps fmaxf: with its statistics the
+  // med3 form spills.)
+  auto vmax = [](float x, float y) __attribute__((always_inline)) {
+    if constexpr (TRAIN) return fmaxf(x, y);
+    return __builtin_amdgcn_fmed3f(x, y, INFINITY);
+  };
+  auto pooled_row = [&](int pi, f32x4 (&carry)[4][4], f32x4 (&next)[4][4]) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);  // the two rows of a pair do not interleave (register pressure)
     const int py = py0 + pi;
-    // vertical max over conv rows 2py-1, 2py, 2py+1 (carry holds 2py-1)
+    // vertical max over conv rows 2py-1 (carry), 2py, 2py+1 (next)
     conv_row(2 * py, cur);
     if (TRAIN) train_row(cur);
+    // max with the carried row BEFORE the next row's MFMAs, so the carried row
+    // is dead during them (a fused 3-way max after them kept all three rows
+    // live: 254 VGPRs and register copies)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cur[i][j][e] = vmax(carry[i][j][e], cur[i][j][e]);
+      }
+    conv_row(2 * py + 1, next);
+    if (TRAIN) train_row(next);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) cur[i][j][e] = fmaxf(carry[i][j][e], cur[i][j][e]);
-    conv_row(2 * py + 1, carry);
-    if (TRAIN) train_row(carry);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cur[i][j][e] = fmaxf(cur[i][j][e], carry[i][j][e]);
+        for (int e = 0; e < 4; ++e) cur[i][j][e] = vmax(cur[i][j][e], next[i][j][e]);
     // wave edge: conv column 64w-1 comes from wave w-1 (tile 3, lanes fg = 3, element 3)
     if (fg == 3) {
 #pragma unroll
@@ -800,11 +816,12 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
         float left = __int_as_float(__builtin_amdgcn_ds_bpermute(((lane + 48) & 63) << 2, __float_as_int(send)));
         if (i == 0 && fg == 0) left = wave > 0 ? s_edge[(wave - 1) * 64 + j * 16 + fr] : -INFINITY;
         if constexpr (!X3 && !TRAIN) {
-          // bias already in the accumulators: pooled pixels q0 = 32w+8i+2fg and
-          // q0 + 1 of channel c = 16j + fr packed as one bf16 pair, ReLU on the
+          // pooled pixels q0 = 32w+8i+2fg and q0 + 1 of channel c = 16j + fr,
+          // plus the bias, packed as one bf16 pair, ReLU on the
           // pair (int16 max), then lanes (c, c^1) trade pairs (one DPP) and a
           // byte permute forms (c0, c0+1) of q0 (even lanes) / q0+1 (odd)
-          const uint32_t pq = stem_relu2(stem_pk(fmaxf(fmaxf(left, x[0]), x[1]), fmaxf(fmaxf(x[1], x[2]), x[3])));
+          const uint32_t pq = stem_relu2(stem_pk(fmaxf(fmaxf(left, x[0]), x[1]) + bias[j],
+                                                 fmaxf(fmaxf(x[1], x[2]), x[3]) + bias[j]));
           const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pq, 0xB1, 0xF, 0xF, true);  // quad_perm 1,0,3,2
           const uint32_t w = __builtin_amdgcn_perm(pn, pq, even ? 0x05040100u : 0x03020706u);
           const int q = wave * 32 + i * 8 + 2 * fg + (even ? 0 : 1);
@@ -843,6 +860,21 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void stem_bf16_kernel(StemArgs a) 
       *(uint4*)(out + idx) = *(const uint4*)(s_out + px * OPITCH + ((X3 ? c : c ^ stem_oswz(px)) << 4));
     }
     __syncthreads();
+  };
+  static_assert(STEM_P % 2 == 0, "pooled rows in pairs");
+  if constexpr (TRAIN) {  // (the statistics' registers: one row per iteration, the carry copied)
+    for (int pi = 0; pi < STEM_P; ++pi) {
+      pooled_row(pi, ca, cb);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ca[i][j] = cb[i][j];
+    }
+  } else {
+    for (int pi = 0; pi < STEM_P; pi += 2) {
+      pooled_row(pi, ca, cb);
+      pooled_row(pi + 1, cb, ca);
+    }
   }
   if constexpr (TRAIN) {
     // lanes (fr, fg = 0..3) share channels 16j + fr: fold fg, then the 4 waves
