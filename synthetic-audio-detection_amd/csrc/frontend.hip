@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <functional>
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -47,6 +48,8 @@ struct FrontendPlan {
   float2* d_tw1024 = nullptr;  // e^{-2 pi i m / 1024}, m < 1024
   float2* d_tw2048 = nullptr;  // e^{-2 pi i k / 2048}, k <= 1024
   float* d_window = nullptr;   // periodic Hann(2048)
+  float* d_window_s16 = nullptr;  // the same times 2^-15 (int16 PCM: torchaudio.load's 1/32768, folded)
+  float2* d_rtw = nullptr;     // [FE_NC + 1] real-spectrum recovery twiddle of bin k (fe_rtw_kernel)
   int* d_mel_start = nullptr;  // [n_mels] first bin
   int* d_mel_len = nullptr;    // [n_mels]
   int* d_mel_off = nullptr;    // [n_mels] offset into d_mel_w
@@ -70,6 +73,19 @@ constexpr int kNormRegs = 32;    // normalisation: values per thread of 1,024 (m
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// e^{-2 pi i k / 2048} of the real-spectrum recovery, k = 0..1024: the
+// 1024-point table at k / 2, times e^{-2 pi i / 2048} for odd k (the per-bin
+// arithmetic fe_mel_db_kernel ran per frame until round 6, now once per plan)
+__device__ __forceinline__ float2 fe_rtw(const float2* tw1024, int k) {
+  float2 w2 = tw1024[(k >> 1) & (FE_NC - 1)];
+  if (k == FE_NC) w2 = make_float2(-1.f, 0.f);
+  if (k & 1) w2 = cmul(w2, make_float2(0.99999529380957619f, -0.0030679567629659761f));
+  return w2;
+}
+__global__ void fe_rtw_kernel(const float2* __restrict__ tw1024, float2* __restrict__ rtw) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k <= FE_NC) rtw[k] = fe_rtw(tw1024, k);
 }
 
 // ---- four-step 1024-point FFT building blocks (one wave per frame) ----------
@@ -120,8 +136,10 @@ constexpr int FE_STAGE_MELS = 128;  // dB rows staged in LDS for coalesced store
 constexpr int FE_POW = 800;         // power bins per wave in LDS (the reference's bank: 767)
 constexpr int FE_PWPAD = 8;         // zero slots before bin_lo (the mel windows' shifted starts)
 constexpr int FE_ZBUF = FE_NC + 16;  // spectrum slots per wave (fe_zslot padding)
-// LDS: twiddles 8 KB + 4 FFT buffers 32.5 KB + power 12.5 KB + dB staging 16.5 KB
-// = 70 KB: two workgroups per CU.  (The mel weights are read from the lane
+constexpr int FE_RTWN = 784;         // recovery twiddles held in LDS (the reference's bank: 767 bins)
+// LDS: recovery twiddles 6.1 KB + 4 FFT buffers 32.5 KB + power 12.5 KB + dB
+// staging 16.5 KB = 68 KB: two workgroups per CU (the frame-major form, without
+// the staging: 52 KB, three).  (The mel weights are read from the lane
 // table in global memory, L1-resident: 11.5 KB for the reference's bank.)
 
 // The fused form's tail: the segment's last workgroup standardises it.  The
@@ -206,36 +224,39 @@ __device__ __forceinline__ void fe_standardise_segment(float* db, bool keep_db, 
   }
 }
 
-// FM (frame-major, round 6, SAD_FE_FM=1, off by default): the dB map goes out
-// as [seg][frame][mel] -- each frame's 128 values are one 512-B row, so a lane
-// stores its mel rows straight from registers -- and fe_normalize_fm transposes
-// it while standardising.  Without the dB staging (16.9 KB) and the LDS twiddle
-// table (8 KB; read from global memory instead) a workgroup needs 46.6 KB of
-// LDS, so three fit on a CU and each SIMD holds three waves
-// (__launch_bounds__(256, 3): 168 VGPRs, 28 B of spills, no prefetch pipeline).
-// Measured slower: 2.89 vs 1.97 ms per 2,048 segments (same box, 3 rounds,
-// profiles/r06_ab_nopk.log) -- the third wave does not buy back the pipeline
-// and the re-read twiddles.  Bit-identical to the default form
+// FM (frame-major, round 6, the default; SAD_FE_FM=0 selects the staged
+// form): the dB map goes out as [seg][frame][mel] -- each frame's 128 values
+// are one 512-B row, so a lane stores its mel rows straight from registers --
+// and fe_normalize_fm transposes it while standardising.  Without the dB
+// staging (16.9 KB) a workgroup needs 52 KB of LDS, so three fit on a CU and
+// each SIMD holds three waves (__launch_bounds__(256, 3): 154 VGPRs, no
+// spills, the PCM prefetch kept; the step-2 twiddles and the window are
+// re-read per frame).  With the per-bin recovery twiddles tabled per plan
+// (fe_rtw) it runs at 1.62-1.66 ms per 2,048 segments against the staged
+// form's 1.85-1.88 and round 6's first 1.97 (same box, 3 rounds,
+// profiles/r06_fe_fm_ab.log).  Bit-identical to the staged form
 // (tests/test_gpu_frontend_fused.py).
 template <typename IT, bool FM = false>  // int16_t PCM (scaled by 1/32768, torchaudio.load normalize) or float
 __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
     const IT* __restrict__ pcm, int64_t seg_stride, const int64_t* __restrict__ seg_offs, int64_t max_off,
     int n_samples,
     int n_frames, int hop,
-    const float2* __restrict__ tw1024, const float* __restrict__ window, const int* __restrict__ mel_start,
+    const float2* __restrict__ tw1024, const float2* __restrict__ rtw, const float* __restrict__ window,
+    const int* __restrict__ mel_start,
     const int* __restrict__ mel_len, const int* __restrict__ mel_off, const float* __restrict__ mel_w, int nnz,
     int n_mels, int bin_lo, int bin_hi, const int* __restrict__ lane_tab, const float* __restrict__ lane_w, int ml0,
     int ml1, float* __restrict__ out, int64_t n_seg, int xcd_map, int fuse, float top_db, float* __restrict__ map_out,
     unsigned* __restrict__ seg_cnt, float* __restrict__ seg_bmax) {
-  __shared__ float2 s_tw[FM ? 1 : FE_NC];
+  // recovery twiddles of bins bin_lo.. (FE_RTWN of them; a wider bank reads them from global memory)
+  __shared__ float2 s_rtw[FE_RTWN];
   __shared__ float2 s_buf[FE_WAVES][FE_ZBUF];
   __shared__ float2 s_tw3[64];  // W64^{q k2} at [k2][q]
   __shared__ float s_pow[FE_WAVES][FE_POW];
   __shared__ float s_db[FM ? 1 : FE_STAGE_MELS][FE_FRAMES_PER_WG + 1];
   __shared__ double s_red[16];
   __shared__ int s_last;
-  // the twiddle table: LDS (two-workgroup form) or global memory (FM)
-  auto twl = [&](int i) __attribute__((always_inline)) { return FM ? tw1024[i] : s_tw[i]; };
+  // the 1024-point twiddle table (register and LDS tables' set-up, FM's step 2)
+  auto twl = [&](int i) __attribute__((always_inline)) { return tw1024[i]; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // 1-D grid.  xcd_map: workgroup L -> segment 8 (L / 8 / n_fb) + L % 8, frame
@@ -256,12 +277,14 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
     x0 = o < 0 ? 0 : (o > max_off ? max_off : o);
   }
   const IT* x = pcm + x0;
-  const float in_scale = sizeof(IT) == 2 ? (1.0f / 32768.0f) : 1.0f;
+  // (int16: the window carries torchaudio.load's 1/32768 -- a power of two, so
+  // e * (w / 32768) rounds exactly as (e / 32768) * w)
   // staged: the mel rows by lane table (plan_create builds it when n_mels <=
   // FE_STAGE_MELS and the padded rows fit the power buffer), dB rows through LDS
   const bool staged = FM || lane_w != nullptr;
-  if constexpr (!FM)
-    for (int i = tid; i < FE_NC; i += 256) s_tw[i] = tw1024[i];
+  const bool rtw_lds = bin_hi - bin_lo < FE_RTWN;  // uniform
+  if (rtw_lds)
+    for (int i = tid; i <= bin_hi - bin_lo; i += 256) s_rtw[i] = rtw[bin_lo + i];
   // this lane's mel rows (staged path) from the lane table: mm = the row (-1:
   // none), mk0 = its first bin - bin_lo; the power buffer's tail past bin_hi is
   // read (times a zero weight) by the padded rows: zero it once, the frames
@@ -307,9 +330,9 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
   // transformed (software pipeline: a frame's HBM latency no longer stalls its
   // wave).  The prefetch address is clamped into the segment, so it is always
   // valid; frames needing reflection (the first / last ones) take the slow path.
-  // (FM: no software pipeline -- the third wave per SIMD hides the latency, and
-  // the 32 registers of the in-flight frame are what the occupancy needs)
-  constexpr bool PREF = sizeof(IT) == 2 && !FM;
+  // (FM too since round 6: without the per-frame twiddle arithmetic the form
+  // needs 154 VGPRs with the pipeline, inside its three-wave budget of 168)
+  constexpr bool PREF = sizeof(IT) == 2;
   uint32_t pre[PREF ? 16 : 1];
   auto frame_inside = [&](int tt) { return pairs && tt * hop - pad >= 0 && tt * hop - pad + FE_NFFT <= n_samples; };
   auto prefetch = [&](int tt) __attribute__((always_inline)) {
@@ -372,7 +395,7 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
           e1 = (float)x[i1];
         }
         const float2 wv = wvs[b + 4 * r];
-        x16[b + 4 * r] = make_float2(e0 * in_scale * wv.x, e1 * in_scale * wv.y);
+        x16[b + 4 * r] = make_float2(e0 * wv.x, e1 * wv.y);
       }
     }
     // ---- four-step FFT, N = 16 x 64: Z[k1 + 16 k2] = sum_l W64^{l k2} W1024^{l k1}
@@ -415,23 +438,28 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
     // a wrong bin 705 beside the stem; the cause was the packed-FP32
     // instructions, which the library no longer uses: csrc/Makefile NOPK)
     const int n_kit = (bin_hi - bin_lo + 64) / 64;
-    for (int it = 0; it < n_kit; ++it) {
-      const int k_raw = bin_lo + lane + 64 * it;
-      const int k = k_raw <= bin_hi ? k_raw : bin_hi;
-      const float2 A = buf[fe_zslot(k & (FE_NC - 1))];
-      const float2 Bc = buf[fe_zslot((FE_NC - k) & (FE_NC - 1))];
-      const float2 B = make_float2(Bc.x, -Bc.y);              // conj(Z[N/2-k])
-      const float2 E = make_float2(0.5f * (A.x + B.x), 0.5f * (A.y + B.y));
-      const float2 D = make_float2(A.x - B.x, A.y - B.y);
-      const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);  // -i/2 (A - B)
-      // e^{-2 pi i k / 2048}: the 1024-point table at k/2, times e^{-2 pi i / 2048} for odd k
-      float2 w2 = twl((k >> 1) & (FE_NC - 1));
-      if (k == FE_NC) w2 = make_float2(-1.f, 0.f);
-      if (k & 1) w2 = cmul(w2, make_float2(0.99999529380957619f, -0.0030679567629659761f));
-      const float2 WO = cmul(w2, O);
-      const float re = E.x + WO.x, im = E.y + WO.y;
-      if (k_raw <= bin_hi) pw[k - bin_lo + FE_PWPAD] = re * re + im * im;
-    }
+    // e^{-2 pi i k / 2048} of bin k (fe_rtw, tabled per plan): from LDS, or
+    // from global memory for a bank wider than FE_RTWN bins (two loop copies:
+    // a select between the two loads issued both)
+    auto recover = [&](auto from_lds) __attribute__((always_inline)) {
+      for (int it = 0; it < n_kit; ++it) {
+        const int k_raw = bin_lo + lane + 64 * it;
+        const int k = k_raw <= bin_hi ? k_raw : bin_hi;
+        const float2 A = buf[fe_zslot(k & (FE_NC - 1))];
+        const float2 Bc = buf[fe_zslot((FE_NC - k) & (FE_NC - 1))];
+        const float2 B = make_float2(Bc.x, -Bc.y);              // conj(Z[N/2-k])
+        const float2 E = make_float2(0.5f * (A.x + B.x), 0.5f * (A.y + B.y));
+        const float2 D = make_float2(A.x - B.x, A.y - B.y);
+        const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);  // -i/2 (A - B)
+        const float2 WO = cmul(decltype(from_lds)::value ? s_rtw[k - bin_lo] : rtw[k], O);
+        const float re = E.x + WO.x, im = E.y + WO.y;
+        if (k_raw <= bin_hi) pw[k - bin_lo + FE_PWPAD] = re * re + im * im;
+      }
+    };
+    if (rtw_lds)
+      recover(std::true_type{});
+    else
+      recover(std::false_type{});
     wave_lds_sync();
     if (staged) {
       // every lane runs ml0 + ml1 steps (no divergence, independent loads):
@@ -901,6 +929,13 @@ static int frontend_plan_build(const sad_frontend_cfg* cfg, const float* fb_in, 
   UP(p->d_tw1024, tw);
   UP(p->d_tw2048, tw2);
   UP(p->d_window, win);
+  std::vector<float> win16(FE_NFFT);
+  for (int n = 0; n < FE_NFFT; ++n) win16[n] = win[n] * (1.0f / 32768.0f);  // exact: a power of two
+  UP(p->d_window_s16, win16);
+  SAD_CHECK_HIP(hipMalloc((void**)&p->d_rtw, (FE_NC + 1) * sizeof(float2)));
+  hipLaunchKernelGGL(fe_rtw_kernel, dim3((FE_NC + 256) / 256), dim3(256), 0, 0, p->d_tw1024, p->d_rtw);
+  SAD_CHECK_HIP(hipGetLastError());
+  SAD_CHECK_HIP(hipStreamSynchronize(nullptr));
   UP(p->d_mel_start, st);
   UP(p->d_mel_len, ln);
   UP(p->d_mel_off, off);
@@ -937,6 +972,8 @@ extern "C" int sad_frontend_plan_destroy(sad_frontend_plan* p) {
   (void)hipFree(p->d_tw1024);
   (void)hipFree(p->d_tw2048);
   (void)hipFree(p->d_window);
+  (void)hipFree(p->d_window_s16);
+  (void)hipFree(p->d_rtw);
   (void)hipFree(p->d_mel_start);
   (void)hipFree(p->d_mel_len);
   (void)hipFree(p->d_mel_off);
@@ -964,12 +1001,12 @@ static int fe_xcd_map() {
   return v;
 }
 
-// SAD_FE_FM=1: the frame-major form (three workgroups per CU, measured slower;
-// see fe_mel_db_kernel) instead of the two-kernel staged form
+// SAD_FE_FM (default 1): the frame-major form (three workgroups per CU; see
+// fe_mel_db_kernel); 0: the staged form (dB rows through LDS, two per CU)
 static int fe_fm() {
   static const int v = [] {
     const char* e = getenv("SAD_FE_FM");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
@@ -1007,7 +1044,8 @@ static int frontend_run(const sad_frontend_plan* p, const IT* pcm, int64_t n_seg
     auto kfn = fm ? fe_mel_db_kernel<IT, true> : fe_mel_db_kernel<IT, false>;
     hipLaunchKernelGGL(kfn, dim3(blocks), dim3(256), 0, s,
                        seg_offs ? pcm : pcm + done * seg_stride, seg_stride, seg_offs ? seg_offs + done : nullptr,
-                       max_off, p->cfg.n_samples, p->n_frames, p->cfg.hop_length, p->d_tw1024, p->d_window,
+                       max_off, p->cfg.n_samples, p->n_frames, p->cfg.hop_length, p->d_tw1024, p->d_rtw,
+                       sizeof(IT) == 2 ? p->d_window_s16 : p->d_window,
                        p->d_mel_start, p->d_mel_len, p->d_mel_off, p->d_mel_w, p->nnz, p->cfg.n_mels, p->bin_lo,
                        p->bin_hi, p->d_lane_tab, p->d_lane_w, p->ml0, p->ml1, dbbuf + off, chunk, xmap, fuse, p->cfg.top_db,
                        out_map + off, p->d_seg_cnt, p->d_seg_bmax);

@@ -1,9 +1,9 @@
 """GPU: the experimental one-kernel front end (SAD_FE_FUSED=1 fences / 2
 agent-scope stores: fe_mel_db's last workgroup per segment standardises the
 segment, csrc/frontend.hip) and the XCD-ordered grid (SAD_FE_XCD_MAP=1) against
-the default two-kernel form, bit for bit; so is round 6's frame-major form
-(SAD_FE_FM=1: fe_mel_db<IT, true> + fe_normalize_fm, three workgroups per CU,
-the transpose in the normalisation; measured slower, off by default).  The settings are read once per
+the default form, bit for bit.  Since round 6 the default is the frame-major
+form (fe_mel_db<IT, true> + fe_normalize_fm, three workgroups per CU, the
+transpose in the normalisation); SAD_FE_FM=0 is the staged two-kernel form.  The settings are read once per
 process, so child processes compute the alternatives.  Cases: ragged batch
 sizes (the XCD-ordered grid is padded to a multiple of 8 segments), the
 clamped-dB output, the windows entry point, and a repeated launch (the fused
@@ -60,10 +60,10 @@ def _ours():
 
 @pytest.mark.parametrize('env', [{'SAD_FE_FUSED': '1'}, {'SAD_FE_FUSED': '2'},
                                  {'SAD_FE_FUSED': '2', 'SAD_FE_XCD_MAP': '1'}, {'SAD_FE_XCD_MAP': '1'},
-                                 {'SAD_FE_FM': '1'}])
+                                 {'SAD_FE_FM': '0'}])
 def test_frontend_forms_equal_default(tmp_path, env):
     for k in ('SAD_FE_FUSED', 'SAD_FE_XCD_MAP', 'SAD_FE_FM'):
-        assert os.environ.get(k, '0') == '0', 'this test runs the default form in-process'
+        assert k not in os.environ, 'this test runs the default form in-process'
     path = str(tmp_path / 'alt.npz')
     code = CHILD.format(root=ROOT, pkg=os.path.join(ROOT, 'synthetic-audio-detection_amd'), sizes=SIZES, path=path)
     r = subprocess.run([sys.executable, '-c', code], env=dict(os.environ, **env), capture_output=True, text=True,
