@@ -136,12 +136,21 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   };
 
   // ---- patch pieces of chunk c of tile t into buffer buf: piece q = wave + 8k
-  // (k = -1: all of this wave's pieces); the tile origin is wave-uniform
-  auto issue_patch = [&](int t, int c, int buf, int k_only) __attribute__((always_inline)) {
-    if (t >= tp_end) return;
+  // (k = -1: all of this wave's pieces); the tile origin is wave-uniform and
+  // decoded once per chunk (TileO), not per piece
+  struct TileO {
+    int b, oy0, ox0;
+    bool ok;
+  };
+  auto tile_o = [&](int t) __attribute__((always_inline)) {
     const int tt = __builtin_amdgcn_readfirstlane(t);
     const int b = tt / tiles_img, rem = tt - b * tiles_img;
-    const int oy0 = (rem / tiles_x) * TH, ox0 = (rem - (rem / tiles_x) * tiles_x) * TW;
+    const int ty = rem / tiles_x;
+    return TileO{b, ty * TH, (rem - ty * tiles_x) * TW, tt < tp_end};
+  };
+  auto issue_patch = [&](const TileO& to, int c, int buf, int k_only) __attribute__((always_inline)) {
+    if (!to.ok) return;
+    const int b = to.b, oy0 = to.oy0, ox0 = to.ox0;
     int lr;  // opaque lane row: keeps the per-piece (py, px) from being hoisted into registers
     asm volatile("v_mov_b32 %0, %1" : "=v"(lr) : "v"(lrow));
     const unsigned dst = lds0 + buf * PATCH;
@@ -177,7 +186,7 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
   // ---- prologue loads: the first chunk's patch, step 0's weights, the bias of
   // this lane's channels (every tile's accumulators start at the bias: the
   // epilogue adds nothing)
-  issue_patch(tp_begin, 0, 0, -1);
+  issue_patch(tile_o(tp_begin), 0, 0, -1);
   f32x4 biasv[TC];
 #pragma unroll
   for (int i = 0; i < TC; ++i) biasv[i] = *(const f32x4*)(a.bias + cw + i * 16 + fg * 4);
@@ -343,6 +352,7 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
       const bool sc = c >= nc0;
       const int nsteps = sc ? 1 : 9;
       const int nt = c + 1 < nch ? t : t + 1, ncn = c + 1 < nch ? c + 1 : 0;  // next chunk
+      const TileO nto = tile_o(nt);
       const int pbuf = u & 1;
       for (int tap = 0; tap < nsteps; ++tap) {
         if (tap == 0) {
@@ -364,9 +374,9 @@ __global__ __launch_bounds__(512, 1) void halo256r_kernel(BlockConvArgs a) {
           if (!(ab & 4)) load_w(kbn, wnxt);
           if (ab & 2) {
           } else if (sc) {
-            issue_patch(nt, ncn, pbuf ^ 1, -1);  // waited for at the next step (a chunk start)
+            issue_patch(nto, ncn, pbuf ^ 1, -1);  // waited for at the next step (a chunk start)
           } else if (tap >= 1 && tap <= 6) {
-            issue_patch(nt, ncn, pbuf ^ 1, tap - 1);
+            issue_patch(nto, ncn, pbuf ^ 1, tap - 1);
           }
         }
         const int ky = sc ? 0 : tap / 3, kx = sc ? 0 : tap - 3 * (tap / 3);
