@@ -121,7 +121,10 @@ __device__ __forceinline__ void dft16(float2 (&x)[16]) {
 }
 // spectrum slot of bin k in the wave's buffer: 4 pad slots per 256 bins make the
 // final scatter (k = k1 + 16 k2a + 256 br(q)) bank-conflict-free
-__device__ __forceinline__ int fe_zslot(int k) { return k + 4 * (k >> 8); }
+// (one pad slot per 64 bins: the scatter's lane groups land on the same banks as
+// with four per 256, and bins k + 64 are always 65 slots on, so the recovery
+// walks its two spectrum reads by constant strides)
+__device__ __forceinline__ int fe_zslot(int k) { return k + (k >> 6); }
 
 // LDS exchange between the lanes of ONE wave: the wave's LDS operations
 // complete in order, so a compiler fence at wavefront scope is all that is
@@ -441,25 +444,43 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
     // e^{-2 pi i k / 2048} of bin k (fe_rtw, tabled per plan): from LDS, or
     // from global memory for a bank wider than FE_RTWN bins (two loop copies:
     // a select between the two loads issued both)
-    auto recover = [&](auto from_lds) __attribute__((always_inline)) {
+    // FAST (twiddles in LDS, bins 1..1023: no wrap of k or N/2 - k): bin k + 64
+    // reads slots 65 on / 65 back and twiddle / power slots 64 on, so every
+    // address is a per-lane base plus a constant; lanes past bin_hi read
+    // unclamped (garbage, in or past the workgroup's LDS: zero) and store nothing
+    auto recover = [&](auto from_lds, auto fast) __attribute__((always_inline)) {
+      constexpr bool FAST = decltype(fast)::value;
+      const float2* pa = buf + fe_zslot(bin_lo + lane);
+      const float2* pb = buf + fe_zslot(FE_NC - bin_lo - lane);
       for (int it = 0; it < n_kit; ++it) {
         const int k_raw = bin_lo + lane + 64 * it;
-        const int k = k_raw <= bin_hi ? k_raw : bin_hi;
-        const float2 A = buf[fe_zslot(k & (FE_NC - 1))];
-        const float2 Bc = buf[fe_zslot((FE_NC - k) & (FE_NC - 1))];
-        const float2 B = make_float2(Bc.x, -Bc.y);              // conj(Z[N/2-k])
-        const float2 E = make_float2(0.5f * (A.x + B.x), 0.5f * (A.y + B.y));
+        const int k = FAST ? k_raw : (k_raw <= bin_hi ? k_raw : bin_hi);
+        const float2 A = FAST ? pa[65 * it] : buf[fe_zslot(k & (FE_NC - 1))];
+        const float2 Bc = FAST ? pb[-65 * it] : buf[fe_zslot((FE_NC - k) & (FE_NC - 1))];
+        const float2 B = make_float2(Bc.x, -Bc.y);  // conj(Z[N/2-k])
+        // 2 X_k = (A + B) - i W (A - B): the recovery's 1/2 factors are left
+        // out (exact powers of two), so pw holds 4 |X_k|^2 and the mel weights
+        // carry the 1/4 -- the same bits as before, four VALU fewer per bin
+        // (the fused operations spelled out as the compiler formed them with
+        // the halvings in place: W O with O = -i (A - B), then each half-sum
+        // added -- so every rounding is the earlier one's, times 2)
+        const float2 E = make_float2(A.x + B.x, A.y + B.y);
         const float2 D = make_float2(A.x - B.x, A.y - B.y);
-        const float2 O = make_float2(0.5f * D.y, -0.5f * D.x);  // -i/2 (A - B)
-        const float2 WO = cmul(decltype(from_lds)::value ? s_rtw[k - bin_lo] : rtw[k], O);
-        const float re = E.x + WO.x, im = E.y + WO.y;
-        if (k_raw <= bin_hi) pw[k - bin_lo + FE_PWPAD] = re * re + im * im;
+        const float ox = D.y, oy = -D.x;  // O = -i (A - B)
+        const float2 w2 = decltype(from_lds)::value ? s_rtw[k - bin_lo] : rtw[k];
+        const float wy_oy = w2.y * oy, wy_ox = w2.y * ox;
+        const float wox = __builtin_fmaf(w2.x, ox, -wy_oy), woy = __builtin_fmaf(w2.x, oy, wy_ox);
+        const float re = E.x + wox, im = E.y + woy;
+        const float im2 = im * im;
+        if (k_raw <= bin_hi) pw[k - bin_lo + FE_PWPAD] = __builtin_fmaf(re, re, im2);
       }
     };
-    if (rtw_lds)
-      recover(std::true_type{});
+    if (rtw_lds && bin_lo >= 1 && bin_hi < FE_NC)
+      recover(std::true_type{}, std::true_type{});
+    else if (rtw_lds)
+      recover(std::true_type{}, std::false_type{});
     else
-      recover(std::false_type{});
+      recover(std::false_type{}, std::false_type{});
     wave_lds_sync();
     if (staged) {
       // every lane runs ml0 + ml1 steps (no divergence, independent loads):
@@ -807,7 +828,10 @@ static int frontend_plan_build(const sad_frontend_cfg* cfg, const float* fb_in, 
     st[m] = a;
     ln[m] = b - a + 1;
     off[m] = (int)w.size();
-    for (int k = a; k <= b; ++k) w.push_back(fb[(size_t)k * cfg->n_mels + m]);
+    // x 1/4: the kernels' power is 4 |X_k|^2 (the real-spectrum recovery's two
+    // halvings dropped); both factors are powers of two, so every product and
+    // sum of the projection rounds exactly as before
+    for (int k = a; k <= b; ++k) w.push_back(0.25f * fb[(size_t)k * cfg->n_mels + m]);
     lo = std::min(lo, a);
     hi = std::max(hi, b);
   }
