@@ -261,7 +261,10 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
   // the 1024-point twiddle table (register and LDS tables' set-up, FM's step 2)
   auto twl = [&](int i) __attribute__((always_inline)) { return tw1024[i]; };
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (the wave index through readfirstlane: the compiler then knows every
+  // per-frame quantity -- t, its PCM base, the reflection test -- is uniform and
+  // keeps it in SGPRs with scalar branches)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // 1-D grid.  xcd_map: workgroup L -> segment 8 (L / 8 / n_fb) + L % 8, frame
   // block (L / 8) % n_fb, so a segment's blocks share L mod 8 (one XCD);
   // else segment L / n_fb, block L % n_fb
@@ -335,22 +338,29 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
   // valid; frames needing reflection (the first / last ones) take the slow path.
   // (FM too since round 6: without the per-frame twiddle arithmetic the form
   // needs 154 VGPRs with the pipeline, inside its three-wave budget of 168)
+  // The loop's prefetch is unconditional (a conditional one joins two paths with
+  // different loads in flight, and the waitcnt pass then waits for all of them
+  // at the next use of an older load): past the last frame it re-reads a clamped
+  // frame, and where the pairs path is off (odd hop or offsets, a segment
+  // shorter than one frame) it reads the window table instead -- never used.
   constexpr bool PREF = sizeof(IT) == 2;
   uint32_t pre[PREF ? 16 : 1];
   auto frame_inside = [&](int tt) { return pairs && tt * hop - pad >= 0 && tt * hop - pad + FE_NFFT <= n_samples; };
+  const bool pf_ok = pairs && n_samples >= FE_NFFT;
+  const IT* pfx = pf_ok ? x : (const IT*)window;  // the window table: 2,048 floats, at least 4 KB
   auto prefetch = [&](int tt) __attribute__((always_inline)) {
     if constexpr (PREF) {
       int b0 = tt * hop - pad;
       b0 = b0 < 0 ? 0 : (b0 + FE_NFFT > n_samples ? (n_samples - FE_NFFT) & ~1 : b0);
-      b0 = b0 < 0 ? 0 : b0;
+      b0 = (b0 < 0 || !pf_ok) ? 0 : b0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int m = lane + 64 * (q & 3) + 256 * (q >> 2);
-        pre[q] = *(const uint32_t*)(x + b0 + 2 * m);
+        pre[q] = *(const uint32_t*)(pfx + b0 + 2 * m);
       }
     }
   };
-  if (PREF && pairs && n_samples >= FE_NFFT) prefetch(f_begin + wave);
+  prefetch(f_begin + wave);
 
   for (int t = f_begin + wave; t < f_end; t += FE_WAVES) {
     // FM: an opaque zero per frame keeps the window and twiddle loads inside
@@ -365,22 +375,48 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
     float2 wvs[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) wvs[q] = *(const float2*)(window + oz + 2 * (lane + 64 * (q & 3) + 256 * (q >> 2)));
-    uint32_t cur[PREF ? 16 : 1];
+    // (one uniform branch around all 16 pairs: per-pair lane masks made the
+    // waitcnt pass wait for every load in flight, the next frame's prefetch
+    // included, at the first pair)
+    // (float PCM keeps the per-pair branch: hoisted, its 16 pair loads spill)
+    auto reflected = [&](int q) __attribute__((always_inline)) {
+      const int m = lane + 64 * (q & 3) + 256 * (q >> 2);
+      int i0 = base + 2 * m, i1 = i0 + 1;
+      i0 = i0 < 0 ? -i0 : i0;
+      i0 = i0 >= n_samples ? 2 * (n_samples - 1) - i0 : i0;
+      i1 = i1 < 0 ? -i1 : i1;
+      i1 = i1 >= n_samples ? 2 * (n_samples - 1) - i1 : i1;
+      x16[q] = make_float2((float)x[i0] * wvs[q].x, (float)x[i1] * wvs[q].y);
+    };
     if constexpr (PREF) {
+      // a frame needing reflection packs its pairs into the prefetch
+      // registers, so both kinds of frame share one conversion (two arms each
+      // converting were merged below the join by 16 register copies)
+      if (!inside) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) cur[q] = pre[q];
-      if (pairs && n_samples >= FE_NFFT && t + FE_WAVES < f_end) prefetch(t + FE_WAVES);
-    }
+        for (int q = 0; q < 16; ++q) {
+          const int m = lane + 64 * (q & 3) + 256 * (q >> 2);
+          int i0 = base + 2 * m, i1 = i0 + 1;
+          i0 = i0 < 0 ? -i0 : i0;
+          i0 = i0 >= n_samples ? 2 * (n_samples - 1) - i0 : i0;
+          i1 = i1 < 0 ? -i1 : i1;
+          i1 = i1 >= n_samples ? 2 * (n_samples - 1) - i1 : i1;
+          pre[PREF ? q : 0] = (uint32_t)(uint16_t)x[i0] | ((uint32_t)(uint16_t)x[i1] << 16);
+        }
+      }
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int j = lane + 64 * b;
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t u = pre[PREF ? q : 0];
+        x16[q] = make_float2((float)(short)(u & 0xFFFF) * wvs[q].x, (float)(short)(u >> 16) * wvs[q].y);
+      }
+    } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = j + 256 * r;
-        float e0, e1;
+      for (int q = 0; q < 16; ++q) {
         if (inside) {
+          const int m = lane + 64 * (q & 3) + 256 * (q >> 2);
+          float e0, e1;
           if constexpr (sizeof(IT) == 2) {
-            const uint32_t u = PREF ? cur[PREF ? b + 4 * r : 0] : *(const uint32_t*)(x + base + 2 * m);
+            const uint32_t u = *(const uint32_t*)(x + base + 2 * m);
             e0 = (float)(short)(u & 0xFFFF);
             e1 = (float)(short)(u >> 16);
           } else {
@@ -388,17 +424,10 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
             e0 = f.x;
             e1 = f.y;
           }
+          x16[q] = make_float2(e0 * wvs[q].x, e1 * wvs[q].y);
         } else {
-          int i0 = base + 2 * m, i1 = i0 + 1;
-          i0 = i0 < 0 ? -i0 : i0;
-          i0 = i0 >= n_samples ? 2 * (n_samples - 1) - i0 : i0;
-          i1 = i1 < 0 ? -i1 : i1;
-          i1 = i1 >= n_samples ? 2 * (n_samples - 1) - i1 : i1;
-          e0 = (float)x[i0];
-          e1 = (float)x[i1];
+          reflected(q);
         }
-        const float2 wv = wvs[b + 4 * r];
-        x16[b + 4 * r] = make_float2(e0 * wv.x, e1 * wv.y);
       }
     }
     // ---- four-step FFT, N = 16 x 64: Z[k1 + 16 k2] = sum_l W64^{l k2} W1024^{l k1}
@@ -412,6 +441,10 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
       x16[fe_p16(k1)] = cmul(x16[fe_p16(k1)], FM ? tw1024[oz + ((lane * k1) & (FE_NC - 1))] : tw2[FM ? 0 : k1]);
 #pragma unroll
     for (int k1 = 0; k1 < 16; ++k1) buf[k1 * 64 + (lane ^ (4 * k1))] = x16[fe_p16(k1)];
+    // the next frame's PCM, into the registers this frame's pairs left (after
+    // the windowing's last use and its path join: no copies, and no wait on
+    // these loads before the next frame)
+    prefetch(t + FE_WAVES);
     wave_lds_sync();
     // lane (g, q) = (lane >> 2, lane & 3): B[l = q + 4 s][k1 = g], s = 0..15
 #pragma unroll
