@@ -125,7 +125,8 @@ __global__ __launch_bounds__(512, 1) void halo256rs2_kernel(BlockConvArgs a) {
   const int cgrp = wave % NCG, pgrp = wave / NCG;
   const int cw = tc * BC + cgrp * 16 * TC;  // this wave's first output channel
   const int r0w = pgrp * TP;                // this wave's first tile row
-  const int ab = a.ablate;  // timing ablations (wrong results): 2 no patch DMA in the loop, 4 no weight loads, 8 no epilogue
+  const int ab = a.ablate;  // timing ablations (wrong results): 2 no patch DMA in the loop, 4 no weight loads, 8 no epilogue,
+                            // 16 no per-plane wait + barrier
 
   const int cinb = a.Cin * 2;
   const int nch = cinb / 128;  // 64-channel (128-B) chunks, 9 taps each
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(512, 1) void halo256rs2_kernel(BlockConvArgs a) {
       const TileO& tn = c + 1 < nch ? tcur : tnext;
 #pragma unroll 1
       for (int T = 0; T < 9; ++T) {
-        if (T == 0 || T == 4 || T == 6 || T == 8) {  // uniform
+        if ((T == 0 || T == 4 || T == 6 || T == 8) && !(ab & 16)) {  // uniform
           if (T == 0 && post_epi)  // the previous tile's stores (youngest) may stay in flight
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"((X3 ? 2 : 1) * TC * TP / 2) : "memory");
           else
