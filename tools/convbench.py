@@ -128,16 +128,17 @@ def bench_blocks(mbs, variants, iters, shapes=None, ablate=(0,), split=False):
             stride = s if sc is None else 1
             flop = 2.0 * mb * Ho * Ho * Cout * K
             ref = None
-            bc = {9: 64, 10: 128, 11: 64, 12: 128, 13: 256, 14: 128, 15: 128, 16: 64, 17: 256, 18: 128, 20: 64, 21: 64, 25: 64, 30: 256, 31: 256, 32: 128, 41: 128, 43: 128, 44: 128}
+            bc = {9: 64, 10: 128, 11: 64, 12: 128, 13: 256, 14: 128, 15: 128, 16: 64, 17: 256, 18: 128, 20: 64, 21: 64, 25: 64, 30: 256, 31: 256, 32: 128, 41: 128, 42: 64, 43: 128, 44: 128}
             for v0 in [v + (ab << 8) for v in variants for ab in ablate]:
                 v = v0 & 255
                 if Cout % bc[v] or (v in (20, 21, 25) and (stride != 1 or sc == 'ds')) or (v == 25 and Cout != 64) or \
                         (v in (30, 31) and (stride != 1 or Ho % 16)) or (v in (32, 44) and (stride != 2 or Ho % 16)) or \
                         (v == 41 and (stride != 1 or Cout != 128 or sc == 'id')) or \
+                        (v == 42 and (stride != 1 or Cout != 64 or sc == 'ds' or not split)) or \
                         (v == 43 and (stride != 2 or Cin != 64 or Cout != 128 or Ho % 16)):
                     continue
                 # the halo kernel (20) takes the identity shortcut as an epilogue residual
-                kw = dict(res=scx) if v in (20, 21, 25) else dict(sc=scx, sc_stride=2 if sc == 'ds' else 1)
+                kw = dict(res=scx) if v in (20, 21, 25, 42) else dict(sc=scx, sc_stride=2 if sc == 'ds' else 1)
                 if sc == 'id' and v == 13 and (v0 >> 8) & 512:
                     kw = dict(res=scx)  # ablate bit 512: the identity as the epilogue residual (RES)
 
