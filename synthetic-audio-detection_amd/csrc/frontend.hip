@@ -749,13 +749,37 @@ __global__ __launch_bounds__(1024) void fe_normalize_fm_kernel(float* db_io, int
   const double var = block_sum_d(ss, red) / (count - 1);
   const float denom = (float)sqrt(var + 0.0) + 1e-6f;
   // frame-major i = frame * n_mels + mel -> mel-major mel * n_frames + frame
+  // (frame / mel of i = tid + 1024 k stepped from k - 1's by the uniform
+  // quotient and remainder of 1024 / n_mels: one integer division per thread)
+  // (the LDS slot m * n_frames + f steps the same way: uniform increments)
+  const int dq = 1024 / n_mels, dr = 1024 - dq * n_mels;
+  const int dslot = dr * n_frames + dq, wrap = n_mels * n_frames - 1;
+  // (v - mean) / denom, correctly rounded without a division per value:
+  // Markstein's step from the correctly rounded reciprocal (q = x y within an
+  // ulp of x / denom, the FMA residual exact, q + r y rounds to x / denom; no
+  // overflow or subnormal range here: |x| >= ulp of a dB value or 0, denom >= 1e-6).
+  // The step turns x = -0 into +0, so the sign is x's (denom > 0).  A CPU check
+  // of 4e8 sampled pairs found no other difference outside subnormal quotients.
+  const float rden = 1.0f / denom;
   auto put = [&](float* dst, bool std) __attribute__((always_inline)) {
+    const int f0 = tid / n_mels, m0 = tid - f0 * n_mels;
+    int m = m0, slot = m0 * n_frames + f0;
 #pragma unroll
     for (int k = 0; k < kNormRegs; ++k) {
-      const int i = tid + k * 1024;
-      if (i < count) {
-        const int f = i / n_mels, m = i - f * n_mels;
-        s_t[m * n_frames + f] = std ? (v[k] - mean_f) / denom : v[k];
+      if (tid + k * 1024 < count) {
+        if (std) {
+          const float xm = v[k] - mean_f;
+          const float q0 = xm * rden;
+          s_t[slot] = __builtin_copysignf(__builtin_fmaf(__builtin_fmaf(-q0, denom, xm), rden, q0), xm);
+        } else {
+          s_t[slot] = v[k];
+        }
+      }
+      slot += dslot;
+      m += dr;
+      if (m >= n_mels) {
+        m -= n_mels;
+        slot -= wrap;
       }
     }
     __syncthreads();
