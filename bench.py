@@ -546,6 +546,11 @@ def main():
                                       'segments_per_s': round(B / (r['fe_ms'] * 1e-3), 1)}},
             'accuracy': accuracy(head),
             'timed_output_check': r['timed_output_check'],
+            # HIP events on the main stream around each stage of the timed steps (means):
+            # front-end wait (overlapped: the side stream's maps), backbone, heads + merge, all-gather
+            'step_breakdown_ms': {'frontend_wait': round(r.get('fe_ms_in_step', r['fe_ms']), 3),
+                                  'backbone': round(r.get('bb_ms_in_step', r['bb_ms']), 3),
+                                  'heads_merge': round(r['heads_ms'], 3), 'allgather': round(r['gather_ms'], 4)},
         }
         if par is not None:
             palg, pexe, pinfo = kernel_roofline(par, 3)
