@@ -379,14 +379,16 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
     // waitcnt pass wait for every load in flight, the next frame's prefetch
     // included, at the first pair)
     // (float PCM keeps the per-pair branch: hoisted, its 16 pair loads spill)
-    auto reflected = [&](int q) __attribute__((always_inline)) {
+    // sample indices of pair q of a frame that needs reflection (center=True
+    // reflect padding at both ends of the segment)
+    auto refl = [&](int q, int& i0, int& i1) __attribute__((always_inline)) {
       const int m = lane + 64 * (q & 3) + 256 * (q >> 2);
-      int i0 = base + 2 * m, i1 = i0 + 1;
+      i0 = base + 2 * m;
+      i1 = i0 + 1;
       i0 = i0 < 0 ? -i0 : i0;
       i0 = i0 >= n_samples ? 2 * (n_samples - 1) - i0 : i0;
       i1 = i1 < 0 ? -i1 : i1;
       i1 = i1 >= n_samples ? 2 * (n_samples - 1) - i1 : i1;
-      x16[q] = make_float2((float)x[i0] * wvs[q].x, (float)x[i1] * wvs[q].y);
     };
     if constexpr (PREF) {
       // a frame needing reflection packs its pairs into the prefetch
@@ -395,12 +397,8 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
       if (!inside) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const int m = lane + 64 * (q & 3) + 256 * (q >> 2);
-          int i0 = base + 2 * m, i1 = i0 + 1;
-          i0 = i0 < 0 ? -i0 : i0;
-          i0 = i0 >= n_samples ? 2 * (n_samples - 1) - i0 : i0;
-          i1 = i1 < 0 ? -i1 : i1;
-          i1 = i1 >= n_samples ? 2 * (n_samples - 1) - i1 : i1;
+          int i0, i1;
+          refl(q, i0, i1);
           pre[PREF ? q : 0] = (uint32_t)(uint16_t)x[i0] | ((uint32_t)(uint16_t)x[i1] << 16);
         }
       }
@@ -409,24 +407,16 @@ __global__ __launch_bounds__(256, FM ? 3 : 2) void fe_mel_db_kernel(
         const uint32_t u = pre[PREF ? q : 0];
         x16[q] = make_float2((float)(short)(u & 0xFFFF) * wvs[q].x, (float)(short)(u >> 16) * wvs[q].y);
       }
-    } else {
+    } else {  // float PCM
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         if (inside) {
-          const int m = lane + 64 * (q & 3) + 256 * (q >> 2);
-          float e0, e1;
-          if constexpr (sizeof(IT) == 2) {
-            const uint32_t u = *(const uint32_t*)(x + base + 2 * m);
-            e0 = (float)(short)(u & 0xFFFF);
-            e1 = (float)(short)(u >> 16);
-          } else {
-            const float2 f = *(const float2*)(x + base + 2 * m);
-            e0 = f.x;
-            e1 = f.y;
-          }
-          x16[q] = make_float2(e0 * wvs[q].x, e1 * wvs[q].y);
+          const float2 f = *(const float2*)(x + base + 2 * (lane + 64 * (q & 3) + 256 * (q >> 2)));
+          x16[q] = make_float2(f.x * wvs[q].x, f.y * wvs[q].y);
         } else {
-          reflected(q);
+          int i0, i1;
+          refl(q, i0, i1);
+          x16[q] = make_float2((float)x[i0] * wvs[q].x, (float)x[i1] * wvs[q].y);
         }
       }
     }
